@@ -1,0 +1,293 @@
+// gpuhash.cpp -- C-ABI host library: contexts, per-device streams, static sharding,
+// launch sequencing and the host argmin.  See include/gpuhash.h for the contract and
+// the reference call sites it replaces.
+#include "gpuhash.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kernels.h"
+#include "plan.h"
+
+using namespace gpuhash;
+
+namespace {
+
+struct Dev {
+    int ord = -1;
+    hipStream_t stream = nullptr;
+    unsigned long long* d_thresh = nullptr;
+    Cand* d_cands = nullptr;
+    unsigned int* d_ncand = nullptr;
+    Cand* d_best = nullptr;
+    Cand* h_best = nullptr;  // pinned
+    uint32_t cap = 0;
+    std::vector<hipEvent_t> ev;
+    // per-call results
+    int rc = GPUHASH_OK;
+    uint64_t best_h = ~0ull, best_n = ~0ull;
+    bool used = false;
+    double kernel_ms = 0;
+    uint32_t launches = 0;
+    std::vector<gpuhash_launch_record> recs;
+};
+
+}  // namespace
+
+struct gpuhash_ctx {
+    std::vector<Dev> devs;
+    gpuhash_stats last{};
+    std::vector<gpuhash_launch_record> recs;
+};
+
+#define HIPCHK(expr)                                \
+    do {                                            \
+        if ((expr) != hipSuccess) return GPUHASH_EHIP; \
+    } while (0)
+
+static int dev_init(Dev& d, int ord) {
+    d.ord = ord;
+    HIPCHK(hipSetDevice(ord));
+    HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    if (hipMalloc(&d.d_thresh, sizeof(unsigned long long)) != hipSuccess) return GPUHASH_ENOMEM;
+    if (hipMalloc(&d.d_ncand, sizeof(unsigned int)) != hipSuccess) return GPUHASH_ENOMEM;
+    if (hipMalloc(&d.d_best, sizeof(Cand)) != hipSuccess) return GPUHASH_ENOMEM;
+    if (hipHostMalloc(&d.h_best, sizeof(Cand), hipHostMallocDefault) != hipSuccess) return GPUHASH_ENOMEM;
+    HIPCHK(hipMemset(d.d_ncand, 0, sizeof(unsigned int)));
+    return GPUHASH_OK;
+}
+
+static void dev_free(Dev& d) {
+    if (d.ord < 0) return;
+    hipSetDevice(d.ord);
+    if (d.stream) hipStreamSynchronize(d.stream);
+    for (auto e : d.ev) hipEventDestroy(e);
+    d.ev.clear();
+    if (d.d_thresh) hipFree(d.d_thresh);
+    if (d.d_ncand) hipFree(d.d_ncand);
+    if (d.d_best) hipFree(d.d_best);
+    if (d.d_cands) hipFree(d.d_cands);
+    if (d.h_best) hipHostFree(d.h_best);
+    if (d.stream) hipStreamDestroy(d.stream);
+    d = Dev{};
+}
+
+static int dev_reserve(Dev& d, uint32_t cap, size_t nev) {
+    if (cap > d.cap) {
+        if (d.d_cands) hipFree(d.d_cands);
+        d.d_cands = nullptr;
+        d.cap = 0;
+        if (hipMalloc(&d.d_cands, (size_t)cap * sizeof(Cand)) != hipSuccess) return GPUHASH_ENOMEM;
+        d.cap = cap;
+    }
+    while (d.ev.size() < nev) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        d.ev.push_back(e);
+    }
+    return GPUHASH_OK;
+}
+
+// Runs one device's shard: every planned launch on the device's stream, a candidate
+// reduce after each, one 16-byte copy back.  mode 1 writes per-nonce hashes to dump.
+static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi,
+                   uint32_t rchunk, int mode, unsigned long long* d_dump) {
+    d.used = true;
+    d.kernel_ms = 0;
+    d.launches = 0;
+    d.recs.clear();
+    HIPCHK(hipSetDevice(d.ord));
+    std::vector<Launch> plan;
+    plan_range(msg, len, lo, hi, plan, rchunk);
+    uint32_t maxb = 1;
+    for (const auto& l : plan) maxb = std::max(maxb, l.nblocks);
+    int rc = dev_reserve(d, maxb, 2 * plan.size());
+    if (rc) return rc;
+    HIPCHK(hipMemsetAsync(d.d_thresh, 0xFF, sizeof(unsigned long long), d.stream));
+    HIPCHK(hipMemsetAsync(d.d_best, 0xFF, sizeof(Cand), d.stream));
+    HIPCHK(hipMemsetAsync(d.d_ncand, 0, sizeof(unsigned int), d.stream));
+    ScanArgs a{d.stream, d.d_thresh, d.d_cands, d.d_ncand, d_dump, (unsigned long long)lo};
+    for (size_t i = 0; i < plan.size(); i++) {
+        HIPCHK(hipEventRecord(d.ev[2 * i], d.stream));
+        HIPCHK(launch_scan(plan[i], mode, a));
+        HIPCHK(hipEventRecord(d.ev[2 * i + 1], d.stream));
+        if (mode == 0) HIPCHK(launch_reduce(d.d_cands, d.d_ncand, d.d_best, d.stream));
+    }
+    HIPCHK(hipMemcpyAsync(d.h_best, d.d_best, sizeof(Cand), hipMemcpyDeviceToHost, d.stream));
+    HIPCHK(hipStreamSynchronize(d.stream));
+    for (size_t i = 0; i < plan.size(); i++) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, d.ev[2 * i], d.ev[2 * i + 1]));
+        d.kernel_ms += ms;
+        const Launch& l = plan[i];
+        d.recs.push_back(gpuhash_launch_record{d.ord, l.J, l.C2, l.EX, l.d, l.c, l.hi - l.lo + 1, (double)ms});
+    }
+    d.launches = (uint32_t)plan.size();
+    d.best_h = d.h_best->hash;
+    d.best_n = d.h_best->nonce;
+    return GPUHASH_OK;
+}
+
+extern "C" {
+
+int gpuhash_open(const int* devices, int ndevices, gpuhash_ctx** out) {
+    if (!out || ndevices < 0 || (ndevices > 0 && !devices)) return GPUHASH_EINVAL;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return GPUHASH_ENODEV;
+    std::vector<int> ords;
+    if (ndevices == 0) {
+        for (int i = 0; i < count; i++) ords.push_back(i);
+    } else {
+        for (int i = 0; i < ndevices; i++) {
+            if (devices[i] < 0 || devices[i] >= count) return GPUHASH_EINVAL;
+            for (int o : ords)
+                if (o == devices[i]) return GPUHASH_EINVAL;
+            ords.push_back(devices[i]);
+        }
+    }
+    for (int o : ords) {  // the code object is gfx950-only
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, o) != hipSuccess) return GPUHASH_ENODEV;
+        if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0) return GPUHASH_ENODEV;
+    }
+    auto* ctx = new gpuhash_ctx();
+    ctx->devs.resize(ords.size());
+    for (size_t i = 0; i < ords.size(); i++) {
+        int rc = dev_init(ctx->devs[i], ords[i]);
+        if (rc) {
+            for (auto& d : ctx->devs) dev_free(d);
+            delete ctx;
+            return rc;
+        }
+    }
+    *out = ctx;
+    return GPUHASH_OK;
+}
+
+int gpuhash_ndevices(const gpuhash_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+
+int gpuhash_min_ex(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uint64_t lower,
+                   uint64_t upper, uint32_t rchunk, uint64_t* out_hash, uint64_t* out_nonce) {
+    if (!ctx || !out_hash || !out_nonce || (msg_len && !msg)) return GPUHASH_EINVAL;
+    if (lower > upper) return GPUHASH_EINVAL;
+    if (msg_len > GPUHASH_MAX_MSG) return GPUHASH_ETOOLONG;
+    auto t0 = std::chrono::steady_clock::now();
+    const int n = (int)ctx->devs.size();
+    std::vector<Shard> sh = shard_range(msg_len, lower, upper, n);
+    for (auto& d : ctx->devs) { d.used = false; d.rc = GPUHASH_OK; d.kernel_ms = 0; d.launches = 0; }
+    if (n == 1) {
+        ctx->devs[0].rc = dev_run(ctx->devs[0], msg, msg_len, lower, upper, rchunk, 0, nullptr);
+    } else {
+        std::vector<std::thread> th;
+        for (int i = 0; i < n; i++) {
+            if (sh[(size_t)i].empty) continue;
+            th.emplace_back([&, i] {
+                Dev& d = ctx->devs[(size_t)i];
+                d.rc = dev_run(d, msg, msg_len, sh[(size_t)i].lo, sh[(size_t)i].hi, rchunk, 0, nullptr);
+            });
+        }
+        for (auto& t : th) t.join();
+    }
+    uint64_t bh = ~0ull, bn = ~0ull;
+    gpuhash_stats st{};
+    bool any = false;
+    ctx->recs.clear();
+    for (auto& d : ctx->devs) {
+        if (!d.used) continue;
+        if (d.rc) return d.rc;
+        // host argmin over the per-device 16-byte results
+        if (!any || d.best_h < bh || (d.best_h == bh && d.best_n < bn)) { bh = d.best_h; bn = d.best_n; }
+        any = true;
+        ctx->recs.insert(ctx->recs.end(), d.recs.begin(), d.recs.end());
+        st.ndevices++;
+        st.launches += d.launches;
+        st.kernel_ms += d.kernel_ms;
+        st.max_dev_kernel_ms = std::max(st.max_dev_kernel_ms, d.kernel_ms);
+    }
+    uint64_t span = upper - lower;
+    st.nonces = span == ~0ull ? ~0ull : span + 1;
+    st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    ctx->last = st;
+    *out_hash = bh;
+    *out_nonce = bn;
+    return GPUHASH_OK;
+}
+
+int gpuhash_min(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uint64_t lower,
+                uint64_t upper, uint64_t* out_hash, uint64_t* out_nonce) {
+    return gpuhash_min_ex(ctx, msg, msg_len, lower, upper, 0, out_hash, out_nonce);
+}
+
+int gpuhash_hash_range(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uint64_t lower,
+                       uint64_t count, uint64_t* out) {
+    if (!ctx || !out || (msg_len && !msg) || ctx->devs.empty()) return GPUHASH_EINVAL;
+    if (count == 0) return GPUHASH_OK;
+    if (count > (1ull << 26) || lower + (count - 1) < lower) return GPUHASH_EINVAL;
+    if (msg_len > GPUHASH_MAX_MSG) return GPUHASH_ETOOLONG;
+    auto t0 = std::chrono::steady_clock::now();
+    Dev& d = ctx->devs[0];
+    for (auto& x : ctx->devs) x.used = false;
+    HIPCHK(hipSetDevice(d.ord));
+    unsigned long long* dd = nullptr;
+    if (hipMalloc(&dd, count * sizeof(uint64_t)) != hipSuccess) return GPUHASH_ENOMEM;
+    int rc = dev_run(d, msg, msg_len, lower, lower + count - 1, 0, 1, dd);
+    if (!rc && hipMemcpy(out, dd, count * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+        rc = GPUHASH_EHIP;
+    hipFree(dd);
+    if (rc) return rc;
+    gpuhash_stats st{};
+    st.nonces = count;
+    st.launches = d.launches;
+    st.ndevices = 1;
+    st.kernel_ms = st.max_dev_kernel_ms = d.kernel_ms;
+    ctx->recs = d.recs;
+    st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    ctx->last = st;
+    return GPUHASH_OK;
+}
+
+uint64_t gpuhash_hash_cpu(const uint8_t* msg, size_t msg_len, uint64_t nonce) {
+    return hash_host(msg, msg_len, nonce);
+}
+
+int gpuhash_last_stats(const gpuhash_ctx* ctx, gpuhash_stats* out) {
+    if (!ctx || !out) return GPUHASH_EINVAL;
+    *out = ctx->last;
+    return GPUHASH_OK;
+}
+
+int gpuhash_last_launches(const gpuhash_ctx* ctx, gpuhash_launch_record* out, int cap) {
+    if (!ctx || cap < 0 || (cap > 0 && !out)) return GPUHASH_EINVAL;
+    const int n = (int)ctx->recs.size();
+    for (int i = 0; i < n && i < cap; i++) out[i] = ctx->recs[(size_t)i];
+    return n;
+}
+
+void gpuhash_close(gpuhash_ctx* ctx) {
+    if (!ctx) return;
+    for (auto& d : ctx->devs) dev_free(d);
+    delete ctx;
+}
+
+const char* gpuhash_strerror(int rc) {
+    switch (rc) {
+        case GPUHASH_OK: return "ok";
+        case GPUHASH_EINVAL: return "invalid argument (null pointer, lower > upper, or bad device list)";
+        case GPUHASH_ENODEV: return "no usable gfx950 (MI355X) device";
+        case GPUHASH_EHIP: return "HIP runtime error or kernel launch failure";
+        case GPUHASH_ETOOLONG: return "message longer than GPUHASH_MAX_MSG";
+        case GPUHASH_ENOMEM: return "out of device or host memory";
+        default: return "unknown gpuhash error";
+    }
+}
+
+const char* gpuhash_version(void) { return "gpuhash 0.1 gfx950"; }
+
+}  // extern "C"

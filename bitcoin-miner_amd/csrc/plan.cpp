@@ -1,0 +1,309 @@
+// plan.cpp -- host-side layout planner (see plan.h for the decomposition).
+//
+// Semantics restated from the reference:
+//   * hashed bytes = msg ‖ 0x20 ‖ decimal(n), "%s %d" of hash.go:13; decimal has no
+//     sign, no padding, "0" for zero, up to 20 digits for a uint64.
+//   * SHA-256 per FIPS 180-4 (Go stdlib crypto/sha256, called at hash.go:12-14).
+//   * result = first 8 digest bytes big-endian = (H0 << 32) | H1 (hash.go:14).
+//   * search range is INCLUSIVE [Lower, Upper] (bitcoin/message.go:25-32, p1.pdf p.14).
+#include "plan.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace gpuhash {
+
+const uint32_t kK[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u,
+    0x923f82a4u, 0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u,
+    0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u, 0xe49b69c1u, 0xefbe4786u,
+    0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+    0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u,
+    0x06ca6351u, 0x14292967u, 0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u,
+    0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u, 0xa2bfe8a1u, 0xa81a664bu,
+    0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+    0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au,
+    0x5b9cca4fu, 0x682e6ff3u, 0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u,
+    0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+
+static inline uint32_t ror(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+void sha256_expand(uint32_t w[64]) {
+    for (int t = 16; t < 64; t++) {
+        uint32_t s0 = ror(w[t - 15], 7) ^ ror(w[t - 15], 18) ^ (w[t - 15] >> 3);
+        uint32_t s1 = ror(w[t - 2], 17) ^ ror(w[t - 2], 19) ^ (w[t - 2] >> 10);
+        w[t] = w[t - 16] + s0 + w[t - 7] + s1;
+    }
+}
+
+void sha256_rounds(uint32_t st[8], const uint32_t w[64], int t_begin, int t_end) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6],
+             h = st[7];
+    for (int t = t_begin; t < t_end; t++) {
+        uint32_t S1 = ror(e, 6) ^ ror(e, 11) ^ ror(e, 25);
+        uint32_t ch = (e & f) ^ (~e & g);
+        uint32_t t1 = h + S1 + ch + kK[t] + w[t];
+        uint32_t S0 = ror(a, 2) ^ ror(a, 13) ^ ror(a, 22);
+        uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+        h = g; g = f; f = e; e = d + t1;
+        d = c; c = b; b = a; a = t1 + S0 + mj;
+    }
+    st[0] = a; st[1] = b; st[2] = c; st[3] = d; st[4] = e; st[5] = f; st[6] = g; st[7] = h;
+}
+
+void sha256_compress(uint32_t st[8], const uint32_t w16[16]) {
+    uint32_t w[64], s[8];
+    std::memcpy(w, w16, 64);
+    sha256_expand(w);
+    std::memcpy(s, st, 32);
+    sha256_rounds(s, w, 0, 64);
+    for (int i = 0; i < 8; i++) st[i] += s[i];
+}
+
+int num_digits(uint64_t n) {
+    int d = 1;
+    while (n >= 10u) { n /= 10u; d++; }
+    return d;
+}
+
+uint64_t pow10u(int k) {
+    uint64_t p = 1;
+    for (int i = 0; i < k; i++) p *= 10u;
+    return p;
+}
+
+uint32_t ascii4(uint32_t x) {
+    uint32_t d0 = x % 10u, d1 = (x / 10u) % 10u, d2 = (x / 100u) % 10u, d3 = (x / 1000u) % 10u;
+    return 0x30303030u | (d3 << 24) | (d2 << 16) | (d1 << 8) | d0;
+}
+
+static inline uint32_t be32(const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+// msg ‖ ' ' ‖ dec(nonce), padded, hashed with this file's compress.  Used for the C-ABI
+// gpuhash_hash_cpu() convenience (the Go shim's one-nonce self-check) only.
+uint64_t hash_host(const uint8_t* msg, uint64_t len, uint64_t nonce) {
+    char dig[20];
+    int nd = 0;
+    uint64_t v = nonce;
+    do { dig[nd++] = (char)('0' + (int)(v % 10u)); v /= 10u; } while (v);
+    uint64_t L = len + 1 + (uint64_t)nd;
+    uint64_t nblk = (L + 9 + 63) / 64;
+    std::vector<uint8_t> buf(nblk * 64, 0);
+    if (len) std::memcpy(buf.data(), msg, len);
+    buf[len] = ' ';
+    for (int i = 0; i < nd; i++) buf[len + 1 + i] = (uint8_t)dig[nd - 1 - i];
+    buf[L] = 0x80;
+    uint64_t bits = L * 8u;
+    for (int i = 0; i < 8; i++) buf[nblk * 64 - 1 - i] = (uint8_t)(bits >> (8 * i));
+    uint32_t st[8];
+    std::memcpy(st, kIV, 32);
+    for (uint64_t b = 0; b < nblk; b++) {
+        uint32_t w[16];
+        for (int i = 0; i < 16; i++) w[i] = be32(&buf[b * 64 + 4 * i]);
+        sha256_compress(st, w);
+    }
+    return ((uint64_t)st[0] << 32) | st[1];
+}
+
+namespace {
+
+struct GroupLayout {
+    int d, J, q, s, C2, EX;
+    uint64_t B;  // index of the block holding the last digit
+};
+
+GroupLayout layout_for(uint64_t m, int d) {
+    GroupLayout g{};
+    g.d = d;
+    uint64_t L = m + 1 + (uint64_t)d;
+    uint64_t f_abs = m + 1, e_abs = L - 1;
+    g.B = e_abs / 64;
+    int e = (int)(e_abs % 64);
+    g.J = e / 4;
+    uint64_t wstart = 64 * g.B + 4 * (uint64_t)g.J;
+    g.q = (int)(e_abs - std::max(wstart, f_abs) + 1);
+    g.EX = e >= 55;
+    int before = d - g.q;
+    g.s = std::min(std::min(kMaxLane, before), kMaxLaunchDigits - g.q);
+    if (g.s < 0) g.s = 0;
+    uint64_t blkB = 64 * g.B;
+    // digit bytes of block B that precede word J
+    uint64_t nbB = (f_abs >= wstart) ? 0 : wstart - std::max(f_abs, blkB);
+    g.C2 = (uint64_t)g.s > nbB;
+    return g;
+}
+
+inline uint32_t low_bytes_mask(int nbytes) {
+    if (nbytes <= 0) return 0u;
+    if (nbytes >= 4) return 0xFFFFFFFFu;
+    return (1u << (8 * nbytes)) - 1u;
+}
+
+void build_launch(const uint8_t* msg, uint64_t m, const GroupLayout& g, uint64_t H,
+                  uint64_t lo, uint64_t hi, uint32_t rchunk_max, Launch& out) {
+    const int d = g.d, q = g.q, s = g.s, h = d - s - q;
+    const uint64_t L = m + 1 + (uint64_t)d;
+    const uint64_t nblk = g.B + 1 + (uint64_t)g.EX;
+    std::vector<uint8_t> buf(nblk * 64, 0);
+    if (m) std::memcpy(buf.data(), msg, m);
+    buf[m] = ' ';
+    // the h leading digits (H has exactly h digits; H == 0 when h == 0)
+    uint64_t v = H;
+    for (int i = h - 1; i >= 0; i--) { buf[m + 1 + (uint64_t)i] = (uint8_t)('0' + v % 10u); v /= 10u; }
+    // lane + loop digit bytes stay 0: the kernel ORs ASCII into them
+    buf[L] = 0x80;
+    uint64_t bits = L * 8u;
+    for (int i = 0; i < 8; i++) buf[nblk * 64 - 1 - (uint64_t)i] = (uint8_t)(bits >> (8 * i));
+    auto words = [&](uint64_t blk, uint32_t w[16]) {
+        for (int i = 0; i < 16; i++) w[i] = be32(&buf[blk * 64 + 4 * (uint64_t)i]);
+    };
+
+    LaunchDesc& D = out.desc;
+    std::memset(&D, 0, sizeof D);
+    uint32_t st[8];
+    std::memcpy(st, kIV, 32);
+    const uint64_t first_var = g.C2 ? g.B - 1 : g.B;
+    for (uint64_t b = 0; b < first_var; b++) {
+        uint32_t w[16];
+        words(b, w);
+        sha256_compress(st, w);
+    }
+    words(g.B, D.U);
+    if (g.C2) {
+        std::memcpy(D.CV1, st, 32);
+        words(g.B - 1, D.U1);
+        uint32_t w[64] = {0};
+        std::memcpy(w, D.U1, 64);  // rounds 0..13 read only W0..W13 (uniform)
+        uint32_t s1[8];
+        std::memcpy(s1, st, 32);
+        sha256_rounds(s1, w, 0, 14);
+        std::memcpy(D.S1, s1, 32);
+    } else {
+        std::memcpy(D.CV, st, 32);
+        uint32_t w[64] = {0};
+        std::memcpy(w, D.U, 64);
+        uint32_t s0[8];
+        std::memcpy(s0, st, 32);
+        if (g.J >= 2) sha256_rounds(s0, w, 0, g.J - 2);
+        std::memcpy(D.S0, s0, 32);
+    }
+    if (g.EX) {
+        uint32_t w[64];
+        words(g.B + 1, w);
+        sha256_expand(w);
+        for (int t = 0; t < 64; t++) D.KWX[t] = kK[t] + w[t];
+    }
+    D.mask_lo = low_bytes_mask(std::min(s, 4));
+    D.mask_hi = low_bytes_mask(s - 4);
+    D.qmask = low_bytes_mask(q);
+    const int e = (int)((L - 1) % 64);
+    D.loop_shift = (uint32_t)(3 - e % 4) * 8u;
+    const uint64_t R = pow10u(q), P = pow10u(s);
+    D.R = (uint32_t)R;
+    uint32_t rc = rchunk_max ? rchunk_max : 100u;
+    D.rchunk = g.C2 ? (uint32_t)R : (uint32_t)std::min<uint64_t>(R, rc);
+    D.nrchunks = (uint32_t)((R + D.rchunk - 1) / D.rchunk);
+    D.p_first = (uint32_t)((lo / R) % P);
+    D.r_first = (uint32_t)(lo % R);
+    D.p_last = (uint32_t)((hi / R) % P);
+    D.r_last = (uint32_t)(hi % R);
+    D.base = H * R * P;
+
+    out.J = g.J; out.C2 = g.C2; out.EX = g.EX;
+    out.d = d; out.q = q; out.s = s;
+    out.c = ((m + 1) / 64 != (L - 1) / 64) ? 2 : 1;
+    out.lo = lo; out.hi = hi;
+    uint32_t npb = (D.p_last - D.p_first) / (uint32_t)kBlock + 1u;
+    out.nblocks = npb * D.nrchunks;
+}
+
+}  // namespace
+
+void plan_range(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper,
+                std::vector<Launch>& out, uint32_t rchunk_max) {
+    const int dlo = num_digits(lower), dhi = num_digits(upper);
+    for (int d = dlo; d <= dhi; d++) {
+        uint64_t a = d == 1 ? 0 : pow10u(d - 1);
+        uint64_t b = d == 20 ? UINT64_MAX : pow10u(d) - 1;
+        a = std::max(a, lower);
+        b = std::min(b, upper);
+        if (a > b) continue;
+        GroupLayout g = layout_for(len, d);
+        const uint64_t U = pow10u(g.s + g.q);
+        const uint64_t Hf = a / U, Hl = b / U;
+        for (uint64_t H = Hf;; H++) {
+            uint64_t lo = std::max(a, H * U);
+            uint64_t hi = (H == Hl) ? b : H * U + (U - 1);
+            Launch l;
+            build_launch(msg, len, g, H, lo, hi, rchunk_max, l);
+            out.push_back(l);
+            if (H == Hl) break;
+        }
+    }
+}
+
+double group_cost(uint64_t msg_len, int d) {
+    GroupLayout g = layout_for(msg_len, d);
+    // relative VALU work per nonce: one final-block compression, +0.7 for the extra
+    // constant block, + the per-lane block B-1 compression amortised over R nonces.
+    double c = 1.0;
+    if (g.EX) c += 0.7;
+    if (g.C2) c += 0.9 / (double)pow10u(g.q);
+    else c += 0.2 / (double)std::min<uint64_t>(pow10u(g.q), 100);
+    return c;
+}
+
+std::vector<Shard> shard_range(uint64_t msg_len, uint64_t lower, uint64_t upper, int n) {
+    std::vector<Shard> sh((size_t)std::max(n, 1));
+    if (n <= 1) { sh[0] = {lower, upper, 0}; return sh; }
+    struct G { uint64_t a, b; long double w; };
+    std::vector<G> gs;
+    long double total = 0;
+    for (int d = num_digits(lower); d <= num_digits(upper); d++) {
+        uint64_t a = d == 1 ? 0 : pow10u(d - 1), b = d == 20 ? UINT64_MAX : pow10u(d) - 1;
+        a = std::max(a, lower); b = std::min(b, upper);
+        if (a > b) continue;
+        long double w = (long double)group_cost(msg_len, d);
+        gs.push_back({a, b, w});
+        total += ((long double)(b - a) + 1.0L) * w;
+    }
+    // cut points: first nonce of shard k (k = 1..n-1) at cumulative cost k·total/n
+    std::vector<uint64_t> cut((size_t)n + 1);
+    cut[0] = lower;
+    size_t gi = 0;
+    long double acc = 0;
+    for (int k = 1; k < n; k++) {
+        long double target = total * (long double)k / (long double)n;
+        while (gi < gs.size()) {
+            long double gc = ((long double)(gs[gi].b - gs[gi].a) + 1.0L) * gs[gi].w;
+            if (acc + gc >= target) break;
+            acc += gc;
+            gi++;
+        }
+        uint64_t c;
+        if (gi >= gs.size()) {
+            c = upper;
+        } else {
+            long double off = (target - acc) / gs[gi].w;
+            uint64_t o = (uint64_t)off;
+            uint64_t span = gs[gi].b - gs[gi].a;
+            if (o > span) o = span;
+            c = gs[gi].a + o;
+        }
+        cut[(size_t)k] = std::max(c, cut[(size_t)k - 1]);
+    }
+    // shard k = [cut[k], cut[k+1]-1]; the last shard ends at upper
+    for (int k = 0; k < n; k++) {
+        uint64_t lo = cut[(size_t)k];
+        if (k == n - 1) { sh[(size_t)k] = {lo, upper, 0}; break; }
+        uint64_t nx = cut[(size_t)k + 1];
+        if (nx == lo) sh[(size_t)k] = {0, 0, 1};
+        else sh[(size_t)k] = {lo, nx - 1, 0};
+    }
+    // the last shard must not be empty-by-overlap: if cut[n-1] > upper cannot happen
+    return sh;
+}
+
+}  // namespace gpuhash

@@ -1,0 +1,104 @@
+// plan.h -- nonce-range planner shared by the HIP host library and the CPU self-check.
+//
+// The reference computes bitcoin.Hash(msg, n) = BE64(SHA256(msg ‖ ' ' ‖ dec(n))[0:8])
+// (src/github.com/cmu440/bitcoin/hash.go:11-15) for every n of the miner's inclusive
+// [Lower, Upper] (bitcoin/message.go:25-32, loop spec'd in p1.pdf pp.12-14) and keeps
+// the least.  The planner turns one such search into launches whose SHA-256 message
+// layout is FIXED per launch, so the kernels can precompute everything that does not
+// depend on the nonce:
+//
+//   digit group   all nonces of one decimal length d (1..20): L = m+1+d hashed bytes
+//   launch        nonces H·10^(s+q) + p·10^q + r sharing the h = d-s-q leading digits H
+//     loop digits r: the q (1..4) digits that sit in the LAST digit-bearing 32-bit word
+//                    W_J of the final block B -> the only per-nonce message word
+//     lane digits p: the s (0..8) digits just before word J, i.e. virtual words J-1 and
+//                    J-2 (these may fall into block B-1: "C2" layouts)
+//     uniform     : prefix bytes, H's digits, 0x80, zero pad, bit length -> host
+//                    precomputes the midstate, the uniform words and the rounds that
+//                    only read uniform words
+//   work item     (a group of 256 consecutive lane values p) × (a chunk of r values)
+//                 = one workgroup of the kernel
+//
+// Kernel variant = (J, C2, EX): J = index of the loop word in block B (0..15);
+// C2 = lane digits spill into block B-1, which is then compressed per lane; EX = the
+// 0x80/length need an extra all-constant block B+1 (last digit at byte >= 55 of B).
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+namespace gpuhash {
+
+static constexpr uint32_t kIV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                                    0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+
+extern const uint32_t kK[64];
+
+// Per-launch constants, passed by value as the kernel argument (lives in SGPRs/
+// the kernarg segment; never touches HBM in the hot loop).  Keep POD + 4-byte words.
+struct LaunchDesc {
+    uint32_t U[16];    // block B words with every lane/loop digit byte zeroed
+    uint32_t S0[8];    // non-C2: block-B state after the uniform rounds 0..J-3
+    uint32_t CV[8];    // non-C2: chaining value entering block B
+    uint32_t U1[16];   // C2: block B-1 words, lane digit bytes zeroed
+    uint32_t S1[8];    // C2: block B-1 state after its uniform rounds 0..13
+    uint32_t CV1[8];   // C2: chaining value entering block B-1
+    uint32_t KWX[64];  // EX: K[t] + W[t] of the all-constant block B+1
+    uint32_t mask_lo;  // bytes of virtual word J-1 that take ascii4(p % 10^4)
+    uint32_t mask_hi;  // bytes of virtual word J-2 that take ascii4(p / 10^4)
+    uint32_t qmask;    // low q bytes
+    uint32_t loop_shift;  // bit position of the last loop digit's byte in W_J
+    uint32_t R;        // 10^q  (r in [0, R))
+    uint32_t rchunk;   // r values per work item
+    uint32_t nrchunks; // ceil(R / rchunk)
+    uint32_t p_first, p_last;  // lane values covered by this launch
+    uint32_t r_first, r_last;  // r bounds at p_first / p_last (edges of [lo, hi])
+    uint32_t pad_;
+    uint64_t base;     // nonce = base + p·R + r
+};
+
+struct Launch {
+    int J;          // loop word index in block B
+    int C2;         // lane block B-1 compressed per lane
+    int EX;         // extra constant padding block
+    int d, q, s;    // digits, loop digits, lane digits
+    int c;          // 64-byte blocks that hold nonce digits (the SURVEY 8(d) "c")
+    uint64_t lo, hi;      // inclusive nonce range covered
+    uint32_t nblocks;     // grid size (workgroups of 256)
+    LaunchDesc desc;
+};
+
+// Largest number of lane digits; 10^kMaxLane lanes per launch.
+static constexpr int kMaxLane = 8;
+static constexpr int kBlock = 256;
+static constexpr int kMaxLaunchDigits = 10;   // s + q <= 10  -> <= 10^10 nonces per launch
+
+// Plans [lower, upper] (inclusive, lower <= upper) of `msg`.  `rchunk_max` caps the r
+// values per work item (0 = default).  Appends to `out`.
+void plan_range(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper,
+                std::vector<Launch>& out, uint32_t rchunk_max = 0);
+
+struct Shard {
+    uint64_t lo, hi;  // inclusive
+    int empty;        // 1 when the range has fewer nonces than shards
+};
+
+// Splits [lower, upper] into n contiguous shards of about equal estimated cost
+// (nonce count weighted by the layout's per-nonce cost).  Used to spread one search
+// over the devices of a context (static contiguous shards).
+std::vector<Shard> shard_range(uint64_t msg_len, uint64_t lower, uint64_t upper, int n);
+
+// Relative per-nonce cost of digit group d for a message of msg_len bytes.
+double group_cost(uint64_t msg_len, int d);
+
+// Host SHA-256 pieces used for midstates (not a hashing path of its own).
+void sha256_compress(uint32_t st[8], const uint32_t w16[16]);
+void sha256_rounds(uint32_t st[8], const uint32_t w[64], int t_begin, int t_end);
+void sha256_expand(uint32_t w[64]);
+uint64_t hash_host(const uint8_t* msg, uint64_t len, uint64_t nonce);
+
+int num_digits(uint64_t n);
+uint64_t pow10u(int k);
+uint32_t ascii4(uint32_t x);  // x < 10^4 -> 4 ASCII digits, big-endian in a word
+
+}  // namespace gpuhash

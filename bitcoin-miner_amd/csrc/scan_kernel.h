@@ -1,0 +1,295 @@
+// scan_kernel.h -- gfx950 nonce-scan kernel template (included by kernels_*.hip).
+//
+// One workgroup = 256 lanes × one chunk of loop values r.  Each lane owns one lane
+// value p (its digits fill message words J-1 / J-2, or block B-1 for C2 layouts) and
+// iterates r (the digits of the LAST digit-bearing word W_J of the final block):
+//
+//   per work item (once):  lane words, the lane-only rounds before J, block B-1 for
+//                           C2, and every schedule/round term that does not read W_J
+//                           (compile-time dependency analysis `kDep` + LICM)
+//   per nonce (hot loop):   W_J = U_J | ascii(r) << shift  -- wave-UNIFORM, SALU
+//                           rounds J..63 on VALU, schedule words that depend on W_J,
+//                           H0 = IV/CV-folded a64; one v_cmp against a wave-uniform
+//                           pruning threshold T; rare slow path does the exact
+//                           lexicographic (hash, nonce) update in scalar registers.
+//
+// Everything is integer VALU: v_alignbit_b32 rotates, v_bitop3_b32 (XOR3 0x96, CH
+// 0xCA, MAJ 0xE8), v_add3_u32.  No LDS or HBM traffic in the loop; one 16-byte
+// candidate per workgroup at the end (appended only if it beats the threshold).
+//
+// Semantics: bitcoin.Hash (src/github.com/cmu440/bitcoin/hash.go:11-15), argmin over
+// the inclusive range with the lowest nonce winning ties (spec'd loop p1.pdf pp.12-14,
+// north_star).  The pruning is exact: T only ever holds the high word of a hash some
+// valid nonce already achieved, and ties on the high word take the slow path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "kernels.h"
+#include "plan.h"
+
+namespace gpuhash {
+
+namespace dev {
+
+__device__ constexpr uint32_t K[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u,
+    0x923f82a4u, 0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u,
+    0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u, 0xe49b69c1u, 0xefbe4786u,
+    0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+    0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u,
+    0x06ca6351u, 0x14292967u, 0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u,
+    0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u, 0xa2bfe8a1u, 0xa81a664bu,
+    0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+    0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au,
+    0x5b9cca4fu, 0x682e6ff3u, 0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u,
+    0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+
+// Per-lane (VGPR) primitives: one VALU op each on gfx950.
+__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) {
+    return __builtin_amdgcn_alignbit(x, x, n);
+}
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t ch(uint32_t e, uint32_t f, uint32_t g) {
+    return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);
+}
+__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+__device__ __forceinline__ uint32_t bS0(uint32_t a) { return xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)); }
+__device__ __forceinline__ uint32_t bS1(uint32_t e) { return xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)); }
+__device__ __forceinline__ uint32_t bs0(uint32_t x) { return xor3(rotr(x, 7), rotr(x, 18), x >> 3); }
+__device__ __forceinline__ uint32_t bs1(uint32_t x) { return xor3(rotr(x, 17), rotr(x, 19), x >> 10); }
+
+// Wave-uniform primitives: plain C so the compiler keeps them on SALU.
+__device__ __forceinline__ uint32_t urotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+__device__ __forceinline__ uint32_t us0(uint32_t x) { return urotr(x, 7) ^ urotr(x, 18) ^ (x >> 3); }
+__device__ __forceinline__ uint32_t us1(uint32_t x) { return urotr(x, 17) ^ urotr(x, 19) ^ (x >> 10); }
+
+__device__ __forceinline__ uint32_t ascii4(uint32_t x) {
+    uint32_t x1 = x / 10u, x2 = x1 / 10u, x3 = x2 / 10u;
+    uint32_t d0 = x - x1 * 10u, d1 = x1 - x2 * 10u, d2 = x2 - x3 * 10u, d3 = x3 % 10u;
+    return 0x30303030u | (d3 << 24) | (d2 << 16) | (d1 << 8) | d0;
+}
+
+// kDep<J>[t]: does schedule word W_t depend on the per-nonce word W_J?
+template <int J>
+struct DepTable {
+    bool v[64];
+    constexpr DepTable() : v() {
+        for (int t = 0; t < 16; t++) v[t] = (t == J);
+        for (int t = 16; t < 64; t++) v[t] = v[t - 2] || v[t - 7] || v[t - 15] || v[t - 16];
+    }
+};
+
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        sfor<B + 1, E>(f);
+    }
+}
+
+struct State {
+    uint32_t a, b, c, d, e, f, g, h;
+};
+
+// One generic round with K[t] + W folded into `kw`.
+__device__ __forceinline__ void round_kw(State& s, uint32_t kw) {
+    uint32_t t1 = s.h + kw + ch(s.e, s.f, s.g) + bS1(s.e);
+    uint32_t t2 = bS0(s.a) + maj(s.a, s.b, s.c);
+    s.h = s.g; s.g = s.f; s.f = s.e; s.e = s.d + t1;
+    s.d = s.c; s.c = s.b; s.b = s.a; s.a = t1 + t2;
+}
+
+// Message expansion of a block whose words are all per-lane or uniform (no W_J):
+// used for block B-1 of C2 layouts, once per work item.
+__device__ __forceinline__ void expand_full(uint32_t (&w)[64]) {
+    sfor<16, 64>([&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        w[t] = w[t - 16] + bs0(w[t - 15]) + w[t - 7] + bs1(w[t - 2]);
+    });
+}
+
+}  // namespace dev
+
+// MODE: 0 = argmin scan (product), 1 = per-nonce hash dump (parity diagnostics).
+template <int J, bool C2, bool EX, int MODE>
+__global__ __launch_bounds__(256) void k_scan(const LaunchDesc D,
+                                              unsigned long long* __restrict__ thresh,
+                                              Cand* __restrict__ cands,
+                                              unsigned int* __restrict__ ncand,
+                                              unsigned long long* __restrict__ dump,
+                                              unsigned long long dump_lo) {
+    using namespace dev;
+    static_assert(J >= 0 && J < 16, "loop word index");
+    static_assert(!C2 || J <= 1, "C2 layouts have the loop word at J <= 1");
+    static_assert(!EX || J >= 13, "extra padding block only when the last digit is at byte >= 55");
+    constexpr DepTable<J> kDep{};
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t item = blockIdx.x;
+    const uint32_t pblk = item / D.nrchunks;
+    const uint32_t rc = item - pblk * D.nrchunks;
+    const uint32_t p = D.p_first + pblk * 256u + tid;
+    const uint32_t r_begin = rc * D.rchunk;
+    const uint32_t r_end = min(r_begin + D.rchunk, D.R);
+
+    // ---- per work item: lane words and everything that does not read W_J ----
+    const uint32_t alo = ascii4(p % 10000u);
+    const uint32_t ahi = ascii4((p / 10000u) % 10000u);
+    uint32_t W[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) W[i] = D.U[i];
+    State s;
+    uint32_t cv[8];
+    if constexpr (C2) {
+        uint32_t V[64];
+#pragma unroll
+        for (int i = 0; i < 16; i++) V[i] = D.U1[i];
+        if constexpr (J == 0) {
+            V[15] |= alo & D.mask_lo;
+            V[14] |= ahi & D.mask_hi;
+        } else {
+            V[15] |= ahi & D.mask_hi;
+            W[0] |= alo & D.mask_lo;
+        }
+        expand_full(V);
+        s = State{D.S1[0], D.S1[1], D.S1[2], D.S1[3], D.S1[4], D.S1[5], D.S1[6], D.S1[7]};
+        sfor<14, 64>([&](auto tc) {
+            constexpr int t = decltype(tc)::value;
+            round_kw(s, K[t] + V[t]);
+        });
+        cv[0] = D.CV1[0] + s.a; cv[1] = D.CV1[1] + s.b; cv[2] = D.CV1[2] + s.c; cv[3] = D.CV1[3] + s.d;
+        cv[4] = D.CV1[4] + s.e; cv[5] = D.CV1[5] + s.f; cv[6] = D.CV1[6] + s.g; cv[7] = D.CV1[7] + s.h;
+        s = State{cv[0], cv[1], cv[2], cv[3], cv[4], cv[5], cv[6], cv[7]};
+        if constexpr (J == 1) round_kw(s, K[0] + W[0]);
+    } else {
+        s = State{D.S0[0], D.S0[1], D.S0[2], D.S0[3], D.S0[4], D.S0[5], D.S0[6], D.S0[7]};
+#pragma unroll
+        for (int i = 0; i < 8; i++) cv[i] = D.CV[i];
+        if constexpr (J >= 2) {
+            W[J - 2] |= ahi & D.mask_hi;
+            W[J - 1] |= alo & D.mask_lo;
+            round_kw(s, K[J - 2] + W[J - 2]);
+            round_kw(s, K[J - 1] + W[J - 1]);
+        } else if constexpr (J == 1) {
+            W[0] |= alo & D.mask_lo;
+            round_kw(s, K[0] + W[0]);
+        }
+    }
+
+    // Edge handling: only the first / last lane of the launch has a partial r range,
+    // and lanes past p_last are idle.  Checked only in the (rare) slow path.
+    const bool lane_ok = p <= D.p_last;
+    const uint32_t rlo = (p == D.p_first) ? D.r_first : 0u;
+    const uint32_t rhi = (p == D.p_last) ? D.r_last : D.R - 1u;
+
+    unsigned long long tv = 0;
+    if constexpr (MODE == 0) tv = __hip_atomic_load(thresh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t T = __builtin_amdgcn_readfirstlane((uint32_t)(tv >> 32));
+    unsigned long long best_h = ~0ull, best_n = ~0ull;
+
+    for (uint32_t r = r_begin; r < r_end; r++) {
+        const uint32_t WJ = D.U[J] | ((ascii4(r) & D.qmask) << D.loop_shift);
+        uint32_t w[64];
+#pragma unroll
+        for (int i = 0; i < 16; i++) w[i] = W[i];
+        w[J] = WJ;
+        // schedule: loop-invariant terms summed first so LICM hoists them
+        sfor<16, 64>([&](auto tc) {
+            constexpr int t = decltype(tc)::value;
+            constexpr bool d2 = kDep.v[t - 2], d7 = kDep.v[t - 7], d15 = kDep.v[t - 15], d16 = kDep.v[t - 16];
+            uint32_t x2, x15;
+            if constexpr (t - 2 == J) x2 = us1(w[t - 2]); else x2 = bs1(w[t - 2]);
+            if constexpr (t - 15 == J) x15 = us0(w[t - 15]); else x15 = bs0(w[t - 15]);
+            uint32_t inv = (d2 ? 0u : x2) + (d7 ? 0u : w[t - 7]) + (d15 ? 0u : x15) + (d16 ? 0u : w[t - 16]);
+            uint32_t var = (d2 ? x2 : 0u) + (d7 ? w[t - 7] : 0u) + (d15 ? x15 : 0u) + (d16 ? w[t - 16] : 0u);
+            w[t] = inv + var;
+        });
+        State x = s;
+        {   // round J: everything but W_J is loop-invariant
+            uint32_t inv = x.h + bS1(x.e) + ch(x.e, x.f, x.g) + K[J];
+            uint32_t t2 = bS0(x.a) + maj(x.a, x.b, x.c);
+            x.h = x.g; x.g = x.f; x.f = x.e; x.e = (x.d + inv) + WJ;
+            x.d = x.c; x.c = x.b; x.b = x.a; x.a = (inv + t2) + WJ;
+        }
+        sfor<J + 1, 63>([&](auto tc) {
+            constexpr int t = decltype(tc)::value;
+            if constexpr (t < 16) round_kw(x, K[t] + w[t]);   // uniform word: K+W folds
+            else round_kw(x, w[t] + K[t]);
+        });
+        uint32_t H0, H1;
+        if constexpr (!EX) {
+            // round 63: e is dead; fold CV0 into the constant so a64 + CV0 is free
+            uint32_t t1 = x.h + w[63] + (K[63] + cv[0]) + ch(x.e, x.f, x.g) + bS1(x.e);
+            H0 = t1 + bS0(x.a) + maj(x.a, x.b, x.c);
+            H1 = cv[1] + x.a;
+        } else {
+            round_kw(x, w[63] + K[63]);
+            State y{cv[0] + x.a, cv[1] + x.b, cv[2] + x.c, cv[3] + x.d,
+                    cv[4] + x.e, cv[5] + x.f, cv[6] + x.g, cv[7] + x.h};
+            const uint32_t y0 = y.a, y1 = y.b;
+            sfor<0, 63>([&](auto tc) {
+                constexpr int t = decltype(tc)::value;
+                round_kw(y, D.KWX[t]);
+            });
+            uint32_t t1 = y.h + D.KWX[63] + ch(y.e, y.f, y.g) + bS1(y.e);
+            H0 = y0 + t1 + bS0(y.a) + maj(y.a, y.b, y.c);
+            H1 = y1 + y.a;
+        }
+
+        if constexpr (MODE == 1) {
+            if (lane_ok && r >= rlo && r <= rhi) {
+                unsigned long long n = D.base + (unsigned long long)p * D.R + r;
+                dump[n - dump_lo] = ((unsigned long long)H0 << 32) | H1;
+            }
+        } else {
+            unsigned long long m = __builtin_amdgcn_ballot_w64(H0 <= T);
+            if (m) {  // wave-uniform, rare once T has settled
+                const bool ok = lane_ok && r >= rlo && r <= rhi;
+                m = __builtin_amdgcn_ballot_w64(H0 <= T && ok);
+                while (m) {
+                    const int l = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const uint32_t h0 = __builtin_amdgcn_readlane(H0, l);
+                    const uint32_t h1 = __builtin_amdgcn_readlane(H1, l);
+                    const uint32_t pl = __builtin_amdgcn_readlane(p, l);
+                    const unsigned long long hh = ((unsigned long long)h0 << 32) | h1;
+                    const unsigned long long nn = D.base + (unsigned long long)pl * D.R + r;
+                    if (hh < best_h || (hh == best_h && nn < best_n)) {
+                        best_h = hh;
+                        best_n = nn;
+                        T = h0 < T ? h0 : T;
+                    }
+                }
+            }
+        }
+    }
+
+    if constexpr (MODE == 0) {
+        __shared__ unsigned long long sh[4][2];
+        const uint32_t wave = tid >> 6;
+        if ((tid & 63u) == 0) { sh[wave][0] = best_h; sh[wave][1] = best_n; }
+        __syncthreads();
+        if (tid == 0) {
+            unsigned long long bh = sh[0][0], bn = sh[0][1];
+#pragma unroll
+            for (int i = 1; i < 4; i++) {
+                if (sh[i][0] < bh || (sh[i][0] == bh && sh[i][1] < bn)) { bh = sh[i][0]; bn = sh[i][1]; }
+            }
+            if (bh != ~0ull || bn != ~0ull) {
+                atomicMin(thresh, bh);
+                const unsigned int idx = atomicAdd(ncand, 1u);
+                cands[idx].hash = bh;
+                cands[idx].nonce = bn;
+            }
+        }
+    }
+}
+
+}  // namespace gpuhash

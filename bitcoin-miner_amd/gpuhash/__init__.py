@@ -1,0 +1,252 @@
+"""gpuhash -- Python host-side mirror of the reference's hot-path interface.
+
+The product is the C-ABI library ``lib/libgpuhash.so`` (include/gpuhash.h) with the
+gfx950 HIP kernels.  This module is a thin ctypes binding over it that mirrors the Go
+names of the reference so tests and bench read like the reference's own code:
+
+  reference (mohitreddy1996/BitCoin-Miner)                 here
+  bitcoin.Hash(msg, nonce)       bitcoin/hash.go:11-15      Hash(msg, nonce)
+  bitcoin.Message/MsgType        bitcoin/message.go:8-21    Message, MsgType
+  bitcoin.NewRequest/NewResult   bitcoin/message.go:25-42   NewRequest, NewResult
+  bitcoin.NewJoin                bitcoin/message.go:45-47   NewJoin
+  miner loop (spec'd, stubbed)   bitcoin/miner/miner.go:15  Miner.handle(request)
+                                 p1.pdf pp.12-14
+
+There is no CPU fallback: if the shared library or a gfx950 device is missing, the
+constructors raise.  (``Hash`` for a single nonce is the host convenience
+gpuhash_hash_cpu, the Go miner's optional self-check -- never used for a search.)
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+import os
+from dataclasses import dataclass
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libgpuhash.so")
+
+GPUHASH_OK = 0
+GPUHASH_EINVAL = -1
+GPUHASH_ENODEV = -2
+GPUHASH_EHIP = -3
+GPUHASH_ETOOLONG = -4
+GPUHASH_ENOMEM = -5
+GPUHASH_MAX_MSG = 1 << 20
+
+# Every symbol include/gpuhash.h declares (tests check the .so exports all of them).
+EXPORTED = [
+    "gpuhash_open", "gpuhash_ndevices", "gpuhash_min", "gpuhash_min_ex",
+    "gpuhash_hash_range", "gpuhash_hash_cpu", "gpuhash_last_stats", "gpuhash_last_launches",
+    "gpuhash_close",
+    "gpuhash_strerror", "gpuhash_version",
+]
+
+
+class GpuHashError(RuntimeError):
+    def __init__(self, rc: int, what: str):
+        self.rc = rc
+        super().__init__(f"{what}: {_lib().gpuhash_strerror(rc).decode()} (rc={rc})")
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("nonces", ctypes.c_uint64),
+        ("launches", ctypes.c_uint32),
+        ("ndevices", ctypes.c_uint32),
+        ("wall_ms", ctypes.c_double),
+        ("kernel_ms", ctypes.c_double),
+        ("max_dev_kernel_ms", ctypes.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+class LaunchRecord(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("device", "J", "C2", "EX", "digits", "c")] + [
+        ("nonces", ctypes.c_uint64), ("ms", ctypes.c_double)]
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+_LIB = None
+
+
+def _lib(path: str | None = None) -> ctypes.CDLL:
+    """Loads libgpuhash.so (raises if it was not built: run __graft_entry__.build())."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError(f"{p} not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(p)
+    u64, sz, u8p = ctypes.c_uint64, ctypes.c_size_t, ctypes.c_char_p
+    vp = ctypes.c_void_p
+    lib.gpuhash_open.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(vp)]
+    lib.gpuhash_open.restype = ctypes.c_int
+    lib.gpuhash_ndevices.argtypes = [vp]
+    lib.gpuhash_ndevices.restype = ctypes.c_int
+    lib.gpuhash_min.argtypes = [vp, u8p, sz, u64, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]
+    lib.gpuhash_min.restype = ctypes.c_int
+    lib.gpuhash_min_ex.argtypes = [vp, u8p, sz, u64, u64, ctypes.c_uint32,
+                                   ctypes.POINTER(u64), ctypes.POINTER(u64)]
+    lib.gpuhash_min_ex.restype = ctypes.c_int
+    lib.gpuhash_hash_range.argtypes = [vp, u8p, sz, u64, u64, vp]
+    lib.gpuhash_hash_range.restype = ctypes.c_int
+    lib.gpuhash_hash_cpu.argtypes = [u8p, sz, u64]
+    lib.gpuhash_hash_cpu.restype = u64
+    lib.gpuhash_last_stats.argtypes = [vp, ctypes.POINTER(Stats)]
+    lib.gpuhash_last_stats.restype = ctypes.c_int
+    lib.gpuhash_last_launches.argtypes = [vp, ctypes.POINTER(LaunchRecord), ctypes.c_int]
+    lib.gpuhash_last_launches.restype = ctypes.c_int
+    lib.gpuhash_close.argtypes = [vp]
+    lib.gpuhash_close.restype = None
+    lib.gpuhash_strerror.argtypes = [ctypes.c_int]
+    lib.gpuhash_strerror.restype = ctypes.c_char_p
+    lib.gpuhash_version.argtypes = []
+    lib.gpuhash_version.restype = ctypes.c_char_p
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+def _bytes(msg) -> bytes:
+    return msg.encode() if isinstance(msg, str) else bytes(msg)
+
+
+class Engine:
+    """One gpuhash context (one or more gfx950 devices)."""
+
+    def __init__(self, devices: list[int] | None = None):
+        lib = _lib()
+        ctx = ctypes.c_void_p()
+        if devices:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            rc = lib.gpuhash_open(arr, len(devices), ctypes.byref(ctx))
+        else:
+            rc = lib.gpuhash_open(None, 0, ctypes.byref(ctx))
+        if rc != GPUHASH_OK:
+            raise GpuHashError(rc, "gpuhash_open")
+        self._ctx = ctx
+
+    @property
+    def ndevices(self) -> int:
+        return _lib().gpuhash_ndevices(self._ctx)
+
+    def min(self, msg, lower: int, upper: int, rchunk: int = 0) -> tuple[int, int]:
+        """argmin over inclusive [lower, upper] of (Hash(msg, n), n)."""
+        m = _bytes(msg)
+        h, n = ctypes.c_uint64(), ctypes.c_uint64()
+        rc = _lib().gpuhash_min_ex(self._ctx, m, len(m), lower, upper, rchunk,
+                                   ctypes.byref(h), ctypes.byref(n))
+        if rc != GPUHASH_OK:
+            raise GpuHashError(rc, "gpuhash_min")
+        return int(h.value), int(n.value)
+
+    def hash_range(self, msg, lower: int, count: int):
+        """numpy uint64 array of Hash(msg, lower + i), computed by the scan kernels."""
+        import numpy as np
+        m = _bytes(msg)
+        out = np.empty(count, dtype=np.uint64)
+        rc = _lib().gpuhash_hash_range(self._ctx, m, len(m), lower, count, out.ctypes.data)
+        if rc != GPUHASH_OK:
+            raise GpuHashError(rc, "gpuhash_hash_range")
+        return out
+
+    def stats(self) -> dict:
+        s = Stats()
+        _lib().gpuhash_last_stats(self._ctx, ctypes.byref(s))
+        return s.as_dict()
+
+    def launches(self) -> list[dict]:
+        """Per-launch records (variant, nonces, HIP-event ms) of the last call."""
+        n = _lib().gpuhash_last_launches(self._ctx, None, 0)
+        arr = (LaunchRecord * max(n, 1))()
+        n = _lib().gpuhash_last_launches(self._ctx, arr, n)
+        return [arr[i].as_dict() for i in range(n)]
+
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            _lib().gpuhash_close(self._ctx)
+            self._ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ---- mirror of the reference's bitcoin package (bitcoin/message.go, hash.go) ----
+
+class MsgType(enum.IntEnum):
+    """bitcoin/message.go:8-12 (iota order)."""
+    Join = 0
+    Request = 1
+    Result = 2
+
+
+@dataclass
+class Message:
+    """bitcoin.Message, message.go:16-21 (JSON field names match Go's)."""
+    Type: MsgType
+    Data: str = ""
+    Lower: int = 0
+    Upper: int = 0
+    Hash: int = 0
+    Nonce: int = 0
+
+    def to_json(self) -> dict:
+        return {"Type": int(self.Type), "Data": self.Data, "Lower": self.Lower,
+                "Upper": self.Upper, "Hash": self.Hash, "Nonce": self.Nonce}
+
+    def __str__(self) -> str:  # Message.String, message.go:49-60
+        if self.Type == MsgType.Request:
+            return f"[Request {self.Data} {self.Lower} {self.Upper}]"
+        if self.Type == MsgType.Result:
+            return f"[Result {self.Hash} {self.Nonce}]"
+        return "[Join]"
+
+
+def NewRequest(data: str, lower: int, upper: int) -> Message:  # message.go:25-32
+    return Message(MsgType.Request, Data=data, Lower=lower, Upper=upper)
+
+
+def NewResult(hash_: int, nonce: int) -> Message:  # message.go:36-42
+    return Message(MsgType.Result, Hash=hash_, Nonce=nonce)
+
+
+def NewJoin() -> Message:  # message.go:45-47
+    return Message(MsgType.Join)
+
+
+def Hash(msg, nonce: int) -> int:
+    """bitcoin.Hash(msg, nonce), hash.go:11-15 (one nonce, host)."""
+    m = _bytes(msg)
+    return int(_lib().gpuhash_hash_cpu(m, len(m), nonce))
+
+
+class Miner:
+    """The miner's Request -> Result step (miner.go:15 TODO; p1.pdf pp.13-14), on GPU.
+
+    Go strings are byte strings: Data is hashed as its UTF-8 bytes, as
+    []byte(fmt.Sprintf("%s %d", ...)) does (hash.go:13).
+    """
+
+    def __init__(self, devices: list[int] | None = None, engine: Engine | None = None):
+        self.engine = engine or Engine(devices)
+
+    def handle(self, req: Message) -> Message:
+        if req.Type != MsgType.Request:
+            raise ValueError(f"miner expects a Request, got {req}")
+        h, n = self.engine.min(req.Data, req.Lower, req.Upper)
+        return NewResult(h, n)

@@ -1,0 +1,123 @@
+/*
+ * gpuhash.h -- C ABI of the MI355X (gfx950) nonce-search engine.
+ *
+ * Drop-in for the ONE hot path of mohitreddy1996/BitCoin-Miner: the miner's min-hash
+ * loop over a Request's inclusive [Lower, Upper].  The reference has no FFI; the
+ * boundary is the Go call site that the unimplemented miner loop would occupy:
+ *
+ *   src/github.com/cmu440/bitcoin/miner/miner.go:15   // TODO: implement this!
+ *     spec (p1.pdf pp.12-14): for n in [Lower, Upper] { h := bitcoin.Hash(Data, n) }
+ *     keep the least h and its nonce, reply bitcoin.NewResult(h, n)
+ *   src/github.com/cmu440/bitcoin/hash.go:11-15        bitcoin.Hash(msg, nonce) uint64
+ *   src/github.com/cmu440/bitcoin/message.go:25-42     NewRequest(data, lower, upper),
+ *                                                      NewResult(hash, nonce)
+ *
+ * A Go miner binds it with cgo (INTEGRATION.md shows the stub).  Plain C types only:
+ * pointers + sizes + uint64; no torch, no HIP types.  All integers host-endian.
+ *
+ * Semantics reproduced bit-exactly:
+ *   Hash(msg, n) = big-endian uint64 of SHA-256(msg ‖ ' ' ‖ decimal(n))[0:8]
+ *   gpuhash_min  = argmin over the INCLUSIVE range of the key (Hash, nonce): the least
+ *                  hash, and among equal hashes the lowest nonce (what an ascending
+ *                  scan with strict '<' returns).  Overflow-safe at upper = 2^64-1.
+ *
+ * Errors are negative return codes (gpuhash_strerror); nothing is printed.  The HIP
+ * path is the only compute path: with no usable device gpuhash_open fails with
+ * GPUHASH_ENODEV -- there is no silent CPU fallback.
+ */
+#ifndef GPUHASH_H
+#define GPUHASH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPUHASH_OK 0
+#define GPUHASH_EINVAL (-1)   /* null pointer, lower > upper, bad device list / count */
+#define GPUHASH_ENODEV (-2)   /* no usable gfx950 device */
+#define GPUHASH_EHIP (-3)     /* a HIP runtime call or kernel launch failed */
+#define GPUHASH_ETOOLONG (-4) /* msg_len > GPUHASH_MAX_MSG */
+#define GPUHASH_ENOMEM (-5)   /* device or host allocation failed */
+
+/* The reference carries the message in a JSON frame inside <=2000-byte LSP datagrams
+ * (lspnet/conn.go:35), so real messages are ~1.3 KB at most; the engine accepts more. */
+#define GPUHASH_MAX_MSG (1u << 20)
+
+typedef struct gpuhash_ctx gpuhash_ctx;
+
+/* Per-call measurements of the last gpuhash_min / gpuhash_hash_range on a context. */
+typedef struct gpuhash_stats {
+    uint64_t nonces;          /* nonces searched by the last call                     */
+    uint32_t launches;        /* scan-kernel launches (all devices)                   */
+    uint32_t ndevices;        /* devices that received a non-empty shard              */
+    double wall_ms;           /* host wall time of the call                           */
+    double kernel_ms;         /* sum over devices of HIP-event time of scan launches  */
+    double max_dev_kernel_ms; /* slowest device's scan-kernel time                    */
+} gpuhash_stats;
+
+/* One scan-kernel launch of the last call (bench.py derives the dominant kernel's
+ * average launch time and algorithmic work from these). */
+typedef struct gpuhash_launch_record {
+    int32_t device;   /* HIP ordinal                                                */
+    int32_t J;        /* kernel variant: loop-word index in the final block (0..15) */
+    int32_t C2;       /* 1: lane digits spill into the previous block               */
+    int32_t EX;       /* 1: extra all-constant padding block                        */
+    int32_t digits;   /* decimal digits of every nonce in the launch                */
+    int32_t c;        /* 64-byte blocks holding nonce digits (1 or 2)               */
+    uint64_t nonces;  /* nonces covered by the launch                               */
+    double ms;        /* HIP-event time of the launch on the device's stream        */
+} gpuhash_launch_record;
+
+/* Opens the listed devices (HIP ordinals); ndevices == 0 means every visible device.
+ * Allocates per-device streams, events and a small candidate buffer.
+ * Replaces: nothing in the reference (the miner would call it once at start-up,
+ * miner.go:8-16). */
+int gpuhash_open(const int *devices, int ndevices, gpuhash_ctx **out);
+
+/* Number of devices a context drives. */
+int gpuhash_ndevices(const gpuhash_ctx *ctx);
+
+/* argmin_{n in [lower, upper]} (Hash(msg, n), n) -> *out_hash, *out_nonce.
+ * Replaces the miner loop of p1.pdf pp.12-14 (miner.go:15) and feeds
+ * bitcoin.NewResult(hash, nonce) (message.go:36-42).  msg is read during the call
+ * only (cgo pointer rules); the range is split statically over the context's devices
+ * (one host thread + one stream each), reduced on the host.  Blocking. */
+int gpuhash_min(gpuhash_ctx *ctx, const uint8_t *msg, size_t msg_len, uint64_t lower,
+                uint64_t upper, uint64_t *out_hash, uint64_t *out_nonce);
+
+/* Same search, caller-chosen work-item granularity (r values per workgroup; 0 =
+ * default).  Exposed for tuning and for parity tests of the chunked paths. */
+int gpuhash_min_ex(gpuhash_ctx *ctx, const uint8_t *msg, size_t msg_len, uint64_t lower,
+                   uint64_t upper, uint32_t rchunk, uint64_t *out_hash, uint64_t *out_nonce);
+
+/* out[i] = Hash(msg, lower + i) for i < count, computed on the first device by the
+ * SAME kernels as gpuhash_min (per-nonce dump mode).  count <= 2^26; lower + count - 1
+ * must not wrap.  Parity/diagnostic API (batch form of hash.go:11-15). */
+int gpuhash_hash_range(gpuhash_ctx *ctx, const uint8_t *msg, size_t msg_len,
+                       uint64_t lower, uint64_t count, uint64_t *out);
+
+/* bitcoin.Hash(msg, nonce) for ONE nonce on the host (hash.go:11-15): the miner's
+ * optional self-check of a returned (hash, nonce); never used by gpuhash_min. */
+uint64_t gpuhash_hash_cpu(const uint8_t *msg, size_t msg_len, uint64_t nonce);
+
+/* Measurements of the last call on ctx. */
+int gpuhash_last_stats(const gpuhash_ctx *ctx, gpuhash_stats *out);
+
+/* Copies up to cap launch records of the last call; returns how many exist. */
+int gpuhash_last_launches(const gpuhash_ctx *ctx, gpuhash_launch_record *out, int cap);
+
+void gpuhash_close(gpuhash_ctx *ctx);
+
+const char *gpuhash_strerror(int rc);
+
+/* Library/ABI version, "gpuhash <major>.<minor> gfx950". */
+const char *gpuhash_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GPUHASH_H */

@@ -1,0 +1,92 @@
+"""CPU: the C-ABI library loads, exports every symbol include/gpuhash.h declares, and
+its host-only pieces behave (no compute call needs a GPU here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "gpuhash.h")
+LIB = os.path.join(ROOT, "bitcoin-miner_amd", "lib", "libgpuhash.so")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        subprocess.check_call(["make", "-C", os.path.join(ROOT, "bitcoin-miner_amd"), "-j4",
+                               "lib/libgpuhash.so"])
+    import gpuhash
+    return gpuhash._lib()
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gpuhash_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_the_boundary():
+    fns = declared_functions()
+    for f in ("gpuhash_open", "gpuhash_min", "gpuhash_hash_cpu", "gpuhash_close", "gpuhash_strerror"):
+        assert f in fns
+
+
+def test_library_exports_every_declared_symbol(lib):
+    import gpuhash
+    fns = declared_functions()
+    assert sorted(gpuhash.EXPORTED) == fns
+    for f in fns:
+        assert hasattr(lib, f), f
+
+
+def test_exports_are_plain_c(lib):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", LIB], text=True)
+    syms = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    for f in declared_functions():
+        assert f in syms, f  # unmangled extern "C"
+
+
+def test_strerror_and_version(lib):
+    assert lib.gpuhash_strerror(0) == b"ok"
+    for rc in (-1, -2, -3, -4, -5):
+        assert lib.gpuhash_strerror(rc) != b"unknown gpuhash error"
+    assert lib.gpuhash_version().startswith(b"gpuhash ")
+
+
+def test_hash_cpu_matches_oracle(lib, oracle):
+    import gpuhash
+    import hash_oracle as ho
+    for m, n, h in ho.SPEC_KATS:
+        assert gpuhash.Hash(m, n) == h
+    for m in (b"", b"bradfitz", b"x" * 55, b"y" * 64, b"z" * 200):
+        for n in (0, 9, 10, 999999999, 10 ** 10, (1 << 64) - 1):
+            assert gpuhash.Hash(m, n) == oracle.hash(m, n)
+
+
+def test_invalid_arguments_rejected_before_any_device_work(lib):
+    h, n = ctypes.c_uint64(), ctypes.c_uint64()
+    assert lib.gpuhash_min(None, b"x", 1, 0, 1, ctypes.byref(h), ctypes.byref(n)) == -1
+    assert lib.gpuhash_open(None, 0, None) == -1
+    assert lib.gpuhash_open(None, -1, ctypes.byref(ctypes.c_void_p())) == -1
+
+
+def test_message_mirror():
+    import gpuhash as g
+    r = g.NewRequest("bradfitz", 0, 9999)
+    assert (r.Type, r.Data, r.Lower, r.Upper) == (g.MsgType.Request, "bradfitz", 0, 9999)
+    assert str(r) == "[Request bradfitz 0 9999]"
+    res = g.NewResult(1419516646206828, 9898)
+    assert str(res) == "[Result 1419516646206828 9898]"
+    assert str(g.NewJoin()) == "[Join]"
+    assert res.to_json()["Type"] == 2
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU is present on this machine")
+def test_no_silent_cpu_fallback(lib):
+    """Without a gfx950 device the engine refuses to open (no CPU fallback)."""
+    import gpuhash
+    with pytest.raises(gpuhash.GpuHashError) as e:
+        gpuhash.Engine()
+    assert e.value.rc == gpuhash.GPUHASH_ENODEV

@@ -1,0 +1,132 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the goldens.
+
+Bar: bit-exact (hash, nonce) for every search and bit-exact per-nonce hashes, on the
+same inputs, at sizes the C oracle finishes in seconds; the committed golden fixtures
+(tests/golden/golden.json, incl. the full 2^32 config-2 range); and at full sizes
+through size-independent properties (split/merge invariance, winner re-hash).
+"""
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+U64 = (1 << 64) - 1
+M120 = (b"The quick brown fox jumps over the lazy dog. " * 3)[:120]
+
+
+def test_spec_kats_through_kernels(engine):
+    # p1.pdf p.12: Hash("msg", 0..2)
+    got = engine.hash_range(b"msg", 0, 3)
+    assert [int(x) for x in got] == [13781283048668101583, 4754799531757243342, 5611725180048225792]
+    assert engine.min(b"msg", 0, 2) == (4754799531757243342, 1)
+
+
+def test_golden_ranges(engine, golden):
+    for r in golden["ranges"]:
+        got = engine.min(bytes.fromhex(r["msg_hex"]), r["lower"], r["upper"])
+        assert got == (r["hash"], r["nonce"]), r["name"]
+
+
+def test_config1_miner_request(engine):
+    import gpuhash as g
+    miner = g.Miner(engine=engine)
+    res = miner.handle(g.NewRequest("bradfitz", 0, 9999))
+    assert (res.Type, res.Hash, res.Nonce) == (g.MsgType.Result, 1419516646206828, 9898)
+    assert g.Hash("bradfitz", res.Nonce) == res.Hash
+
+
+def variant_cases():
+    """(msg, lower, count) windows that straddle digit-count and block boundaries for
+    message lengths 0..140, so every (J, C2, EX) kernel variant and both lane-word
+    placements run."""
+    rng = random.Random(42)
+    cases = []
+    for mlen in list(range(0, 70)) + list(range(100, 141, 3)):
+        m = bytes(rng.randrange(256) for _ in range(mlen))
+        d = rng.choice([3, 5, 7, 9, 10, 11, 12, 13])
+        cases.append((m, 10 ** d - rng.randrange(1, 3000), rng.randrange(1000, 6000)))
+    for m in (b"", b"bradfitz", M120, M120[:44], M120[:45]):
+        cases.append((m, 0, 12000))
+        cases.append((m, U64 - 4999, 5000))
+        cases.append((m, 10 ** 19 - 2500, 5000))
+    return cases
+
+
+def test_hash_range_bit_exact(engine, oracle):
+    for m, lo, cnt in variant_cases():
+        got = engine.hash_range(m, lo, cnt)
+        want = oracle.hash_range(m, lo, cnt)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (len(m), lo, cnt, int(bad[0]) + lo)
+
+
+def test_min_matches_oracle_random(engine, oracle):
+    rng = random.Random(9)
+    for _ in range(120):
+        m = bytes(rng.randrange(256) for _ in range(rng.randrange(0, 160)))
+        kind = rng.randrange(4)
+        if kind == 0:
+            lo = rng.randrange(0, 10 ** rng.randrange(1, 20))
+        elif kind == 1:
+            lo = 10 ** rng.randrange(1, 20) - rng.randrange(0, 50000)
+        elif kind == 2:
+            lo = rng.randrange(0, U64)
+        else:
+            lo = U64 - rng.randrange(0, 100000)
+        lo = max(0, lo)
+        hi = min(U64, lo + rng.randrange(0, 120000))
+        assert engine.min(m, lo, hi) == oracle.min(m, lo, hi), (m, lo, hi)
+
+
+def test_single_nonce_ranges(engine, oracle):
+    rng = random.Random(1)
+    for n in [0, 1, 9, 10, 99, 100, 12345, 10 ** 9 - 1, 10 ** 9, 2 ** 32 - 1, 10 ** 19, U64 - 1, U64] + \
+            [rng.randrange(0, U64) for _ in range(40)]:
+        for m in (b"bradfitz", M120, b""):
+            assert engine.min(m, n, n) == (oracle.hash(m, n), n)
+
+
+@pytest.mark.parametrize("rchunk", [1, 3, 10, 64, 100, 1000, 10000])
+def test_work_item_granularity_is_invisible(engine, oracle, rchunk):
+    for m, lo, hi in [(b"bradfitz", 123456789, 123656789), (M120, 9999990000, 10000040000),
+                      (M120[:45], 999990000, 1000020000), (b"x" * 53, 0, 60000)]:
+        assert engine.min(m, lo, hi, rchunk=rchunk) == oracle.min(m, lo, hi, threads=8)
+
+
+def test_config2_full_range_golden(engine, golden):
+    g = {r["name"]: r for r in golden["ranges"]}["cfg2_bradfitz_2p32"]
+    assert engine.min(b"bradfitz", 0, (1 << 32) - 1) == (g["hash"], g["nonce"])
+    st = engine.stats()
+    assert st["nonces"] == 1 << 32 and st["kernel_ms"] > 0
+
+
+def test_split_merge_invariance_at_scale(engine, oracle):
+    # 2^36 nonces of config-4 shape: the argmin of the whole equals the lexicographic
+    # min of the argmins of any split, and the winner re-hashes to the same value
+    lo, hi = 3 << 36, (4 << 36) - 1
+    whole = engine.min(b"bradfitz", lo, hi)
+    rng = random.Random(4)
+    cut = rng.randrange(lo, hi)
+    parts = [engine.min(b"bradfitz", lo, cut), engine.min(b"bradfitz", cut + 1, hi)]
+    assert whole == min(parts)
+    assert oracle.hash(b"bradfitz", whole[1]) == whole[0]
+    assert lo <= whole[1] <= hi
+
+
+def test_errors_are_loud(engine):
+    import gpuhash
+    with pytest.raises(gpuhash.GpuHashError) as e:
+        engine.min(b"x", 10, 9)
+    assert e.value.rc == gpuhash.GPUHASH_EINVAL
+    with pytest.raises(gpuhash.GpuHashError):
+        gpuhash.Engine([0, 0])
+    with pytest.raises(gpuhash.GpuHashError):
+        engine.hash_range(b"x", U64, 2)  # wraps past 2^64-1
+
+
+def test_native_library_is_the_one_loaded(engine):
+    import gpuhash
+    maps = open("/proc/self/maps").read()
+    assert gpuhash.LIB_PATH in maps

@@ -1,0 +1,147 @@
+"""CPU: the host-side planner (bitcoin-miner_amd/csrc/plan.cpp) without a GPU.
+
+libgpuhash_hostcheck.so exposes the launch plan libgpuhash.so would execute and replays
+the per-nonce data flow of a scan kernel from each launch's descriptor (midstates,
+uniform words, lane/loop digit insertion, extra padding block).  Checked against the
+oracle: exact tiling of [lower, upper], every kernel variant, message lengths across
+block boundaries, digit-count boundaries, and the 2^64-1 edge.
+"""
+import ctypes
+import os
+import random
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIBDIR = os.path.join(ROOT, "bitcoin-miner_amd", "lib")
+HC = os.path.join(LIBDIR, "libgpuhash_hostcheck.so")
+U64 = (1 << 64) - 1
+u64 = ctypes.c_uint64
+
+
+class Info(ctypes.Structure):
+    _fields_ = ([(n, ctypes.c_int) for n in "J C2 EX d q s".split()]
+                + [(n, u64) for n in "lo hi base".split()]
+                + [(n, ctypes.c_uint32) for n in "nblocks R rchunk nrchunks p_first p_last r_first r_last".split()])
+
+
+@pytest.fixture(scope="module")
+def hc():
+    if not os.path.exists(HC):
+        subprocess.check_call(["make", "-C", os.path.join(ROOT, "bitcoin-miner_amd"),
+                               "lib/libgpuhash_hostcheck.so"])
+    lib = ctypes.CDLL(HC)
+    cp, u32 = ctypes.c_char_p, ctypes.c_uint32
+    lib.gpuhash_plan_count.argtypes = [cp, u64, u64, u64, u32]
+    lib.gpuhash_plan_get.argtypes = [cp, u64, u64, u64, u32, ctypes.c_int, ctypes.POINTER(Info)]
+    lib.gpuhash_plan_all.argtypes = [cp, u64, u64, u64, u32, ctypes.POINTER(Info), ctypes.c_int]
+    lib.hostcheck_desc_hash.argtypes = [cp, u64, u64, u64, u32, ctypes.c_int, u64, ctypes.POINTER(u64)]
+    lib.gpuhash_shard.argtypes = [u64, u64, u64, ctypes.c_int, ctypes.POINTER(u64),
+                                  ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_int)]
+    return lib
+
+
+def plan(hc, m, a, b, rchunk=0):
+    n = hc.gpuhash_plan_count(m, len(m), a, b, rchunk)
+    arr = (Info * n)()
+    assert hc.gpuhash_plan_all(m, len(m), a, b, rchunk, arr, n) == n
+    return list(arr)
+
+
+def desc_hash(hc, m, a, b, i, n, rchunk=0):
+    o = u64()
+    assert hc.hostcheck_desc_hash(m, len(m), a, b, rchunk, i, n, ctypes.byref(o)) == 0
+    return o.value
+
+
+def test_plan_tiles_range_and_layouts_are_legal(hc):
+    rng = random.Random(11)
+    for _ in range(600):
+        m = bytes(rng.randrange(256) for _ in range(rng.randrange(0, 200)))
+        a = rng.randrange(0, U64)
+        b = min(U64, a + rng.randrange(0, 10 ** rng.randrange(0, 13)))
+        p = plan(hc, m, a, b)
+        assert p[0].lo == a and p[-1].hi == b
+        for x, y in zip(p, p[1:]):
+            assert y.lo == x.hi + 1
+        for l in p:
+            assert 1 <= l.q <= 4 and 0 <= l.s <= 8 and l.s + l.q <= 10
+            assert not (l.C2 and l.J > 1) and not (l.EX and l.J < 13) and not (l.C2 and l.EX)
+            assert l.R == 10 ** l.q
+            assert l.lo == l.base + l.p_first * l.R + l.r_first
+            assert l.hi == l.base + l.p_last * l.R + l.r_last
+            assert l.nblocks == ((l.p_last - l.p_first) // 256 + 1) * l.nrchunks
+            assert l.nrchunks * l.rchunk >= l.R
+
+
+def test_descriptor_replay_matches_oracle(hc, oracle):
+    rng = random.Random(5)
+    seen = set()
+    for _ in range(1500):
+        m = bytes(rng.randrange(256) for _ in range(rng.randrange(0, 200)))
+        d = rng.randrange(1, 21)
+        lo = 0 if d == 1 else 10 ** (d - 1)
+        hi = min(10 ** d - 1, U64)
+        a = rng.randrange(lo, hi + 1)
+        b = min(hi, a + rng.randrange(0, 10 ** rng.randrange(0, 12)))
+        for i, l in enumerate(plan(hc, m, a, b)):
+            seen.add((l.J, l.C2, l.EX))
+            for n in {l.lo, l.hi, rng.randrange(l.lo, l.hi + 1)}:
+                assert desc_hash(hc, m, a, b, i, n) == oracle.hash(m, n), (m, a, b, i, n)
+    # every one of the 19 reachable (J, C2, EX) variants was exercised
+    assert len(seen) == 19, sorted(seen)
+
+
+@pytest.mark.parametrize("mlen", [0, 8, 44, 45, 53, 54, 55, 56, 63, 64, 110, 119, 120, 127, 128, 180])
+def test_every_digit_count_and_message_length(hc, oracle, mlen):
+    m = bytes((i * 37 + 11) % 256 for i in range(mlen))
+    for d in range(1, 21):
+        lo = 0 if d == 1 else 10 ** (d - 1)
+        hi = min(10 ** d - 1, U64)
+        for a, b in [(lo, min(hi, lo + 1234)), (max(lo, hi - 777), hi)]:
+            for i, l in enumerate(plan(hc, m, a, b)):
+                for n in (l.lo, l.hi):
+                    assert desc_hash(hc, m, a, b, i, n) == oracle.hash(m, n)
+
+
+def test_wide_ranges_plan(hc):
+    for a, b in [(0, (1 << 40) - 1), (0, (1 << 32) - 1), (U64 - 10 ** 12, U64)]:
+        p = plan(hc, b"bradfitz", a, b)
+        assert p[0].lo == a and p[-1].hi == b
+        assert sum(l.hi - l.lo + 1 for l in p) == b - a + 1
+
+
+def test_rchunk_override(hc, oracle):
+    m = b"bradfitz"
+    for rc in (1, 7, 10, 33, 1000):
+        for i, l in enumerate(plan(hc, m, 123456789, 123499999, rc)):
+            assert l.rchunk == (l.R if l.C2 else min(rc, l.R))
+            assert desc_hash(hc, m, 123456789, 123499999, i, l.hi, rc) == oracle.hash(m, l.hi)
+
+
+def shards(hc, mlen, a, b, n):
+    lo, hi, em = (u64 * n)(), (u64 * n)(), (ctypes.c_int * n)()
+    assert hc.gpuhash_shard(mlen, a, b, n, lo, hi, em) == 0
+    return [None if em[i] else (lo[i], hi[i]) for i in range(n)]
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
+def test_shards_tile_range(hc, n):
+    rng = random.Random(n)
+    cases = [(0, (1 << 40) - 1), (0, (1 << 32) - 1), (5, 9), (0, 0), (U64 - 3, U64), (0, U64)]
+    cases += [(x, x + rng.randrange(0, 10 ** 15)) for x in (rng.randrange(0, 10 ** 18) for _ in range(20))]
+    for a, b in cases:
+        s = [x for x in shards(hc, 8, a, b, n) if x is not None]
+        assert s[0][0] == a and s[-1][1] == b
+        for x, y in zip(s, s[1:]):
+            assert y[0] == x[1] + 1
+        assert all(lo <= hi for lo, hi in s)
+
+
+def test_shards_balance_config4(hc):
+    # config 4: [0, 2^40) over 8 GPUs.  d=12 and d=13 layouts cost within a few %,
+    # so the cost-balanced shards hold nearly equal nonce counts
+    s = shards(hc, 8, 0, (1 << 40) - 1, 8)
+    counts = [hi - lo + 1 for lo, hi in s]
+    assert max(counts) / min(counts) < 1.03

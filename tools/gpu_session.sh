@@ -1,0 +1,40 @@
+#!/bin/bash
+# tools/gpu_session.sh STEP... -- runs GPU steps on the gpurun box, each under its own
+# time limit, logging to gpurun_out/.  A plain failure (exit 1, e.g. a failing test)
+# lets the next step run; a fault, abort, segfault, time limit or kill stops the session.
+# Steps: valu | go | test | bench | prof | pmc | scale
+set -u
+cd "$(dirname "$0")/.."
+OUT=gpurun_out
+mkdir -p "$OUT"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+
+run() {  # run <name> <seconds> <cmd...>
+    local name=$1 secs=$2
+    shift 2
+    echo "== $name: $*" | tee -a "$OUT/session.log"
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc" | tee -a "$OUT/session.log"
+    tail -n 5 "$OUT/$name.log"
+    case $rc in
+        0|1|2|5) return 0 ;;
+        *) echo "== stopping: $name ended with rc=$rc" | tee -a "$OUT/session.log"; exit $rc ;;
+    esac
+}
+
+for step in "$@"; do
+    case $step in
+        valu) run valu 90 ./tools/bin/valu_peak 8 100000 ;;
+        go) { command -v go && go version; } > "$OUT/go.log" 2>&1; echo "go: $(cat $OUT/go.log)" ;;
+        test) run pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+        smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        bench) run bench 300 python -u bench.py --steps 10 --warmup 2 ;;
+        prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+        pmc) run pmc_valu 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/pmc1" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
+             run pmc_hbm 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc2" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
+             run pmc_wr 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc3" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+        *) echo "unknown step $step"; exit 2 ;;
+    esac
+done
+echo "== session done"
