@@ -34,6 +34,20 @@ VALU_PEAK_T = 256 * 64 * 2.4e9 / 1e12
 OPS_PER_BLOCK = 1378  # minimal gfx950 VALU ops of one generic SHA-256 compression
 MSG = b"bradfitz"
 PER_GPU = 1 << 32
+M120 = (b"The quick brown fox jumps over the lazy dog. " * 3)[:120]
+# BASELINE.json configs measurable by this script (configs 1 and 5 are LSP plumbing):
+#   2 (headline): 'bradfitz', 2^32 nonces per GPU, weak scaling
+#   3: the 120-byte message over the 9->10 and 10->11 digit windows (2 x (2^29+1) nonces)
+#   4: 'bradfitz', 2^37 nonces per GPU at offset rank*2^37 -> at N=8 exactly [0, 2^40)
+CONFIGS = {
+    "2": {"msg": MSG, "windows": lambda r: [(r * PER_GPU, (r + 1) * PER_GPU - 1)],
+          "desc": "config 2: msg 'bradfitz' (1 SHA block), 2^32 nonces per GPU (rank r: [r*2^32, (r+1)*2^32)), argmin (hash, nonce)"},
+    "3": {"msg": M120, "windows": lambda r: [(10 ** 9 - (1 << 28), 10 ** 9 + (1 << 28)),
+                                             (10 ** 10 - (1 << 28), 10 ** 10 + (1 << 28))],
+          "desc": "config 3: 120-byte msg (3 SHA blocks, host midstate for block 0), windows 10^9 +- 2^28 and 10^10 +- 2^28 per GPU"},
+    "4": {"msg": MSG, "windows": lambda r: [(r << 37, ((r + 1) << 37) - 1)],
+          "desc": "config 4: msg 'bradfitz', 2^37 nonces per GPU (rank r: [r*2^37, (r+1)*2^37)); N=8 covers [0, 2^40)"},
+}
 
 
 def cpu_baseline(seconds: float = 12.0) -> dict:
@@ -57,6 +71,19 @@ def cpu_baseline(seconds: float = 12.0) -> dict:
                       f"{dt:.1f} s; reference Go miner unavailable (no Go toolchain)"}
 
 
+def pmc_traffic(key) -> float | None:
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC
+    summary (profiles/pmc_traffic.json: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE,
+    collected in separate --pmc passes by tools/gpu_session.sh pmc)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        return t["kernels"][f"k_scan<{key[0]}, {bool(key[1])}, {bool(key[2])}, 0>".lower()]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -64,6 +91,7 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--config", default="2", choices=sorted(CONFIGS))
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -79,11 +107,18 @@ def main() -> None:
     import gpuhash
     from gpuhash.dist import gather_results, merge_min, weak_range
     eng = gpuhash.Engine([local])
-    lo, hi = weak_range(0, PER_GPU, rank)
+    cfg = CONFIGS[args.config]
+    msg, windows = cfg["msg"], cfg["windows"](rank)
+    per_gpu = sum(hi - lo + 1 for lo, hi in windows)
     dev = torch.device("cuda", local)
 
-    def step():
-        res = eng.min(MSG, lo, hi)
+    def step(recs=None):
+        parts = []
+        for lo, hi in windows:
+            parts.append(eng.min(msg, lo, hi))
+            if recs is not None:
+                recs.extend(eng.launches())  # HIP-event time of every scan launch
+        res = merge_min(parts)
         if dist is not None:
             res = merge_min(gather_results(res, dev))
         return res
@@ -99,8 +134,7 @@ def main() -> None:
     recs = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        res = step()
-        recs.extend(eng.launches())
+        res = step(recs)
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -123,7 +157,7 @@ def main() -> None:
     kernel_ghs = dom["nonces"] / (dom["ms"] * 1e-3) / 1e9
 
     if rank == 0:
-        total = PER_GPU * world * args.steps
+        total = per_gpu * world * args.steps
         value = total / dt / 1e9
         out = {
             "metric": METRIC,
@@ -137,10 +171,9 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (the nonce space itself; msg 'bradfitz')",
-            "config": {"workload": "config 2: msg 'bradfitz' (1 SHA block), 2^32 nonces per GPU "
-                                   "(rank r: [r*2^32, (r+1)*2^32)), argmin (hash, nonce)",
-                       "msg": MSG.decode(), "nonces_per_gpu": PER_GPU, "parallelism": f"dp{world}"},
+            "data": "synthetic (the nonce space itself; fixed message)",
+            "config": {"workload": cfg["desc"], "msg_len": len(msg), "nonces_per_gpu": per_gpu,
+                       "parallelism": f"dp{world}"},
             "per_gpu_GHs": round(value / world, 4),
             "result_rank0_range": list(res) if world == 1 else None,
             "roofline": {
@@ -149,7 +182,7 @@ def main() -> None:
                 "peak": round(VALU_PEAK_T, 3),
                 "unit": "T int32 lane-ops/s",
                 "frac": round(achieved_T / VALU_PEAK_T, 4),
-                "traffic": None,
+                "traffic": pmc_traffic(key),
                 "kernel": f"k_scan<J={key[0]},C2={key[1]},EX={key[2]},MODE=0>",
                 "avg_launch_ms": round(avg_ms, 4),
                 "nonces_per_launch": dom["nonces"] / dom["n"],
@@ -157,7 +190,7 @@ def main() -> None:
                 "kernel_GHs": round(kernel_ghs, 4),
             },
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.config == "2":
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(out), flush=True)
     eng.close()

@@ -1,0 +1,74 @@
+// Package gpuhash is the cgo binding a maintainer adds next to the reference's
+// src/github.com/cmu440/bitcoin package so the miner's min-hash loop (the TODO at
+// src/github.com/cmu440/bitcoin/miner/miner.go:15, spec'd in p1.pdf pp.12-14) runs on
+// MI355X GPUs through include/gpuhash.h.  bitcoin.Hash (hash.go:11-15) and the
+// Message types (message.go) are untouched.
+//
+// NOT COMPILED IN THIS REPO: neither the build container nor the GPU box has a Go
+// toolchain (DESIGN.md, "Oracle").  Build with:
+//
+//	CGO_CFLAGS="-I<repo>/include" CGO_LDFLAGS="-L<repo>/bitcoin-miner_amd/lib -lgpuhash" go build
+package gpuhash
+
+/*
+#cgo LDFLAGS: -lgpuhash
+#include <stdlib.h>
+#include "gpuhash.h"
+*/
+import "C"
+
+import (
+	"errors"
+	"unsafe"
+)
+
+// Engine owns one gpuhash context (one or more GPUs).
+type Engine struct{ ctx *C.gpuhash_ctx }
+
+func rcErr(rc C.int) error {
+	if rc == C.GPUHASH_OK {
+		return nil
+	}
+	return errors.New(C.GoString(C.gpuhash_strerror(rc)))
+}
+
+// Open opens the given HIP device ordinals (none = every visible device).
+func Open(devices ...int) (*Engine, error) {
+	var ctx *C.gpuhash_ctx
+	var rc C.int
+	if len(devices) == 0 {
+		rc = C.gpuhash_open(nil, 0, &ctx)
+	} else {
+		ds := make([]C.int, len(devices))
+		for i, d := range devices {
+			ds[i] = C.int(d)
+		}
+		rc = C.gpuhash_open(&ds[0], C.int(len(ds)), &ctx)
+	}
+	if err := rcErr(rc); err != nil {
+		return nil, err
+	}
+	return &Engine{ctx: ctx}, nil
+}
+
+// Min returns the least bitcoin.Hash(data, n) over the inclusive [lower, upper] and
+// its nonce (lowest nonce on equal hashes) -- exactly what the spec'd loop
+//
+//	for n := lower; n <= upper; n++ { if h := bitcoin.Hash(data, n); h < best { ... } }
+//
+// returns.  The cgo call releases the P, so LSP's epoch goroutines keep running.
+func (e *Engine) Min(data string, lower, upper uint64) (hash, nonce uint64, err error) {
+	var h, n C.uint64_t
+	var p *C.uint8_t
+	if len(data) > 0 {
+		b := []byte(data) // Go-owned, valid for the duration of the call (cgo rules)
+		p = (*C.uint8_t)(unsafe.Pointer(&b[0]))
+		rc := C.gpuhash_min(e.ctx, p, C.size_t(len(b)), C.uint64_t(lower), C.uint64_t(upper), &h, &n)
+		return uint64(h), uint64(n), rcErr(rc)
+	}
+	rc := C.gpuhash_min(e.ctx, nil, 0, C.uint64_t(lower), C.uint64_t(upper), &h, &n)
+	return uint64(h), uint64(n), rcErr(rc)
+}
+
+// Close releases the devices.
+func (e *Engine) Close() { C.gpuhash_close(e.ctx) }

@@ -46,7 +46,7 @@ def variant_cases():
     for mlen in list(range(0, 70)) + list(range(100, 141, 3)):
         m = bytes(rng.randrange(256) for _ in range(mlen))
         d = rng.choice([3, 5, 7, 9, 10, 11, 12, 13])
-        cases.append((m, 10 ** d - rng.randrange(1, 3000), rng.randrange(1000, 6000)))
+        cases.append((m, max(0, 10 ** d - rng.randrange(1, 3000)), rng.randrange(1000, 6000)))
     for m in (b"", b"bradfitz", M120, M120[:44], M120[:45]):
         cases.append((m, 0, 12000))
         cases.append((m, U64 - 4999, 5000))

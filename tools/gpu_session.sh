@@ -25,7 +25,8 @@ run() {  # run <name> <seconds> <cmd...>
 
 for step in "$@"; do
     case $step in
-        valu) run valu 90 ./tools/bin/valu_peak 8 100000 ;;
+        valu) run valu 120 ./tools/bin/valu_peak 8 50000; run valu1 120 ./tools/bin/valu_peak 1 50000 ;;
+        probe) run probe8 300 ./tools/bin/valu_probe 8 20000 ;;
         go) { command -v go && go version; } > "$OUT/go.log" 2>&1; echo "go: $(cat $OUT/go.log)" ;;
         test) run pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
         smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;

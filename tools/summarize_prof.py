@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Summarise a tools/gpu_session.sh prof+pmc run into profiles/ (committed evidence).
+
+  python tools/summarize_prof.py r01
+writes
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
+  profiles/<tag>_pmc_summary.json   per-kernel counters per launch (VALU, HBM bytes)
+  profiles/pmc_traffic.json         HBM bytes/launch per kernel, read by bench.py
+FETCH_SIZE is doubled: on gfx950 it reports half the bytes of a wide coalesced read
+(/opt/skills/guides/MI355X_MICROARCH.md, HBM section); both are in KB.
+"""
+import collections
+import csv
+import json
+import os
+import re
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "gpurun_out")
+
+
+def short(name: str) -> str:
+    m = re.search(r"(k_scan<[^>]*>|k_reduce|__amd_rocclr_\w+)", name)
+    return m.group(1) if m else name[:60]
+
+
+def load_pmc(d):
+    path = os.path.join(OUT, d, "pmc_counter_collection.csv")
+    if not os.path.exists(path):
+        return {}, {}
+    vals = collections.defaultdict(lambda: collections.defaultdict(float))
+    disp = collections.defaultdict(set)
+    for r in csv.DictReader(open(path)):
+        k = short(r["Kernel_Name"])
+        vals[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        disp[k].add(r["Dispatch_Id"])
+    return vals, {k: len(v) for k, v in disp.items()}
+
+
+def main():
+    tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    stats = os.path.join(OUT, "prof", "bench_kernel_stats.csv")
+    if os.path.exists(stats):
+        shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    summary = {"tag": tag, "kernels": {}}
+    traffic = {"source": f"profiles/{tag}_pmc_summary.json", "kernels": {}}
+    merged = collections.defaultdict(dict)
+    launches = {}
+    for d in ("pmc1", "pmc2", "pmc3"):
+        v, n = load_pmc(d)
+        for k, cs in v.items():
+            for c, x in cs.items():
+                merged[k][c] = x / max(n[k], 1)
+            launches[k] = n[k]
+    for k, cs in merged.items():
+        e = {"launches_profiled": launches.get(k), "per_launch": cs}
+        if "FETCH_SIZE" in cs or "WRITE_SIZE" in cs:
+            hbm = (2.0 * cs.get("FETCH_SIZE", 0.0) + cs.get("WRITE_SIZE", 0.0)) * 1024.0
+            e["hbm_bytes_per_launch"] = hbm
+            traffic["kernels"][k.lower()] = {"hbm_bytes_per_launch": hbm}
+        if "GRBM_GUI_ACTIVE" in cs and "SQ_INSTS_VALU" in cs:
+            e["valu_wave_instr_per_xcd_cycle"] = cs["SQ_INSTS_VALU"] / (cs["GRBM_GUI_ACTIVE"] / 8.0)
+        summary["kernels"][k] = e
+    json.dump(summary, open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w"), indent=1)
+    json.dump(traffic, open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
+    print(json.dumps(summary, indent=1)[:3000])
+
+
+if __name__ == "__main__":
+    main()
