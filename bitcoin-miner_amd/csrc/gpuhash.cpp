@@ -28,6 +28,11 @@ struct Dev {
     Cand* d_best = nullptr;
     Cand* h_best = nullptr;  // pinned
     uint32_t cap = 0;
+    // launch descriptors + prefix offsets + per-launch work counters, staged through a
+    // pinned host buffer and copied once per call
+    uint8_t* d_meta = nullptr;
+    uint8_t* h_meta = nullptr;
+    size_t meta_cap = 0;
     std::vector<hipEvent_t> ev;
     // per-call results
     int rc = GPUHASH_OK;
@@ -74,8 +79,24 @@ static void dev_free(Dev& d) {
     if (d.d_best) hipFree(d.d_best);
     if (d.d_cands) hipFree(d.d_cands);
     if (d.h_best) hipHostFree(d.h_best);
+    if (d.d_meta) hipFree(d.d_meta);
+    if (d.h_meta) hipHostFree(d.h_meta);
     if (d.stream) hipStreamDestroy(d.stream);
     d = Dev{};
+}
+
+static int dev_reserve_meta(Dev& d, size_t bytes) {
+    if (bytes <= d.meta_cap) return GPUHASH_OK;
+    if (d.d_meta) hipFree(d.d_meta);
+    if (d.h_meta) hipHostFree(d.h_meta);
+    d.d_meta = nullptr;
+    d.h_meta = nullptr;
+    d.meta_cap = 0;
+    size_t cap = std::max<size_t>(bytes, 64 * 1024);
+    if (hipMalloc(&d.d_meta, cap) != hipSuccess) return GPUHASH_ENOMEM;
+    if (hipHostMalloc(&d.h_meta, cap, hipHostMallocDefault) != hipSuccess) return GPUHASH_ENOMEM;
+    d.meta_cap = cap;
+    return GPUHASH_OK;
 }
 
 static int dev_reserve(Dev& d, uint32_t cap, size_t nev) {
@@ -94,8 +115,10 @@ static int dev_reserve(Dev& d, uint32_t cap, size_t nev) {
     return GPUHASH_OK;
 }
 
-// Runs one device's shard: every planned launch on the device's stream, a candidate
-// reduce after each, one 16-byte copy back.  mode 1 writes per-nonce hashes to dump.
+// Runs one device's shard.  The planned launches are grouped by kernel variant; each
+// group is ONE persistent launch over all its descriptors (guided self-scheduling, see
+// scan_kernel.h), followed by the candidate reduce.  One 16-byte copy back at the end.
+// mode 1 writes per-nonce hashes to d_dump instead.
 static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi,
                    uint32_t rchunk, int mode, unsigned long long* d_dump) {
     d.used = true;
@@ -105,30 +128,104 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
     HIPCHK(hipSetDevice(d.ord));
     std::vector<Launch> plan;
     plan_range(msg, len, lo, hi, plan, rchunk);
-    uint32_t maxb = 1;
-    for (const auto& l : plan) maxb = std::max(maxb, l.nblocks);
-    int rc = dev_reserve(d, maxb, 2 * plan.size());
+
+    struct Group {
+        int J, C2, EX;
+        std::vector<size_t> idx;
+    };
+    std::vector<Group> groups;
+    for (size_t i = 0; i < plan.size(); i++) {
+        const Launch& l = plan[i];
+        auto it = std::find_if(groups.begin(), groups.end(), [&](const Group& g) {
+            return g.J == l.J && g.C2 == l.C2 && g.EX == l.EX;
+        });
+        if (it == groups.end()) {
+            groups.push_back(Group{l.J, l.C2, l.EX, {}});
+            it = groups.end() - 1;
+        }
+        it->idx.push_back(i);
+    }
+
+    // meta layout: [work counters: 8 B x groups][per group: offs (n+1) x 8 B, descs]
+    size_t bytes = 8 * groups.size();
+    std::vector<size_t> offs_at(groups.size()), desc_at(groups.size());
+    for (size_t g = 0; g < groups.size(); g++) {
+        offs_at[g] = bytes;
+        bytes += 8 * (groups[g].idx.size() + 1);
+        bytes = (bytes + 15) & ~(size_t)15;
+        desc_at[g] = bytes;
+        bytes += sizeof(LaunchDesc) * groups[g].idx.size();
+        bytes = (bytes + 15) & ~(size_t)15;
+    }
+    int rc = dev_reserve_meta(d, bytes);
     if (rc) return rc;
+    std::memset(d.h_meta, 0, 8 * groups.size());
+    uint32_t maxgrid = 1;
+    std::vector<unsigned int> grids(groups.size());
+    for (size_t g = 0; g < groups.size(); g++) {
+        auto* offs = reinterpret_cast<unsigned long long*>(d.h_meta + offs_at[g]);
+        auto* descs = reinterpret_cast<LaunchDesc*>(d.h_meta + desc_at[g]);
+        unsigned long long acc = 0;
+        for (size_t k = 0; k < groups[g].idx.size(); k++) {
+            const LaunchDesc& D = plan[groups[g].idx[k]].desc;
+            offs[k] = acc;
+            acc += (unsigned long long)((D.p_last - D.p_first) / (uint32_t)kBlock + 1u) * D.R;
+            descs[k] = D;
+        }
+        offs[groups[g].idx.size()] = acc;
+        unsigned int full = grid_for(groups[g].J, groups[g].C2, groups[g].EX, mode, d.ord);
+        if (full == 0) return GPUHASH_EHIP;
+        // no more workgroups than minimum-size pieces
+        unsigned long long pieces = (acc + 9) / 10;
+        grids[g] = (unsigned int)std::min<unsigned long long>(full, std::max<unsigned long long>(pieces, 1));
+        maxgrid = std::max(maxgrid, grids[g]);
+    }
+    rc = dev_reserve(d, maxgrid, 2 * groups.size());
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(d.d_meta, d.h_meta, bytes, hipMemcpyHostToDevice, d.stream));
     HIPCHK(hipMemsetAsync(d.d_thresh, 0xFF, sizeof(unsigned long long), d.stream));
     HIPCHK(hipMemsetAsync(d.d_best, 0xFF, sizeof(Cand), d.stream));
     HIPCHK(hipMemsetAsync(d.d_ncand, 0, sizeof(unsigned int), d.stream));
-    ScanArgs a{d.stream, d.d_thresh, d.d_cands, d.d_ncand, d_dump, (unsigned long long)lo};
-    for (size_t i = 0; i < plan.size(); i++) {
-        HIPCHK(hipEventRecord(d.ev[2 * i], d.stream));
-        HIPCHK(launch_scan(plan[i], mode, a));
-        HIPCHK(hipEventRecord(d.ev[2 * i + 1], d.stream));
+    const unsigned int gmax = rchunk ? rchunk : 400u;
+    const unsigned int gmin = std::min(10u, gmax);
+    for (size_t g = 0; g < groups.size(); g++) {
+        ScanArgs a{};
+        a.stream = d.stream;
+        a.descs = reinterpret_cast<const LaunchDesc*>(d.d_meta + desc_at[g]);
+        a.offs = reinterpret_cast<const unsigned long long*>(d.d_meta + offs_at[g]);
+        a.ndesc = (int)groups[g].idx.size();
+        a.work = reinterpret_cast<unsigned long long*>(d.d_meta + 8 * g);
+        a.gmin = gmin;
+        a.gmax = gmax;
+        a.thresh = d.d_thresh;
+        a.cands = d.d_cands;
+        a.ncand = d.d_ncand;
+        a.dump = d_dump;
+        a.dump_lo = lo;
+        a.grid = grids[g];
+        HIPCHK(hipEventRecord(d.ev[2 * g], d.stream));
+        HIPCHK(launch_scan(groups[g].J, groups[g].C2, groups[g].EX, mode, a));
+        HIPCHK(hipEventRecord(d.ev[2 * g + 1], d.stream));
         if (mode == 0) HIPCHK(launch_reduce(d.d_cands, d.d_ncand, d.d_best, d.stream));
     }
     HIPCHK(hipMemcpyAsync(d.h_best, d.d_best, sizeof(Cand), hipMemcpyDeviceToHost, d.stream));
     HIPCHK(hipStreamSynchronize(d.stream));
-    for (size_t i = 0; i < plan.size(); i++) {
+    for (size_t g = 0; g < groups.size(); g++) {
         float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, d.ev[2 * i], d.ev[2 * i + 1]));
+        HIPCHK(hipEventElapsedTime(&ms, d.ev[2 * g], d.ev[2 * g + 1]));
         d.kernel_ms += ms;
-        const Launch& l = plan[i];
-        d.recs.push_back(gpuhash_launch_record{d.ord, l.J, l.C2, l.EX, l.d, l.c, l.hi - l.lo + 1, (double)ms});
+        uint64_t nonces = 0, biggest = 0;
+        const Launch* big = nullptr;
+        for (size_t k : groups[g].idx) {
+            const Launch& l = plan[k];
+            uint64_t n = l.hi - l.lo + 1;
+            nonces += n;
+            if (!big || n > biggest) { big = &l; biggest = n; }
+        }
+        d.recs.push_back(gpuhash_launch_record{d.ord, groups[g].J, groups[g].C2, groups[g].EX,
+                                               big->d, big->c, nonces, (double)ms});
     }
-    d.launches = (uint32_t)plan.size();
+    d.launches = (uint32_t)groups.size();
     d.best_h = d.h_best->hash;
     d.best_n = d.h_best->nonce;
     return GPUHASH_OK;
@@ -288,6 +385,12 @@ const char* gpuhash_strerror(int rc) {
     }
 }
 
-const char* gpuhash_version(void) { return "gpuhash 0.1 gfx950"; }
+const char* gpuhash_version(void) {
+#ifdef GPUHASH_TIE_TEST_BITS
+    return "gpuhash 0.2 gfx950 TIE-TEST (truncated keys; test build only)";
+#else
+    return "gpuhash 0.2 gfx950";
+#endif
+}
 
 }  // extern "C"

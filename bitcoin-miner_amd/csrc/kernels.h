@@ -14,15 +14,24 @@ struct Cand {
 
 struct ScanArgs {
     hipStream_t stream;
-    unsigned long long* thresh;  // pruning threshold (monotone atomicMin), per job
-    Cand* cands;                 // appended per-workgroup candidates
-    unsigned int* ncand;         // append counter
-    unsigned long long* dump;    // MODE 1 only: per-nonce hashes
-    unsigned long long dump_lo;  // MODE 1 only: nonce of dump[0]
+    const LaunchDesc* descs;         // device: the group's launch descriptors
+    const unsigned long long* offs;  // device: ndesc+1 prefix offsets in row-iterations
+    int ndesc;
+    unsigned long long* work;        // device: guided-scheduling counter (zeroed per launch)
+    unsigned int gmin, gmax;         // piece size bounds (r values per grab)
+    unsigned long long* thresh;      // pruning threshold (monotone atomicMin), per job
+    Cand* cands;                     // appended per-workgroup candidates
+    unsigned int* ncand;             // append counter
+    unsigned long long* dump;        // MODE 1 only: per-nonce hashes
+    unsigned long long dump_lo;      // MODE 1 only: nonce of dump[0]
+    unsigned int grid;               // workgroups (<= resident capacity, see grid_for)
 };
 
-// mode 0 = argmin scan, 1 = per-nonce hash dump
-hipError_t launch_scan(const Launch& l, int mode, const ScanArgs& a);
+// Resident workgroups of 256 threads for the (J, C2, EX, mode) kernel on this device.
+unsigned int grid_for(int J, int C2, int EX, int mode, int device);
+
+// One persistent launch of the (J, C2, EX) variant over a.descs[0..ndesc).
+hipError_t launch_scan(int J, int C2, int EX, int mode, const ScanArgs& a);
 hipError_t launch_reduce(Cand* cands, unsigned int* ncand, Cand* best, hipStream_t stream);
 
 }  // namespace gpuhash

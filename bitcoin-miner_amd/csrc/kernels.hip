@@ -40,52 +40,94 @@ __global__ __launch_bounds__(1024) void k_reduce(Cand* __restrict__ cands,
 }
 
 template <int J, bool C2, bool EX, int MODE>
-static hipError_t go(const Launch& l, const ScanArgs& a) {
-    hipLaunchKernelGGL((k_scan<J, C2, EX, MODE>), dim3(l.nblocks), dim3(256), 0, a.stream, l.desc,
-                       a.thresh, a.cands, a.ncand, a.dump, a.dump_lo);
+static auto kfn() {
+    return &k_scan<J, C2, EX, MODE>;
+}
+
+template <int J, bool C2, bool EX, int MODE>
+static hipError_t go(const ScanArgs& a) {
+    hipLaunchKernelGGL((k_scan<J, C2, EX, MODE>), dim3(a.grid), dim3(256), 0, a.stream, a.descs,
+                       a.offs, a.ndesc, a.work, a.gmin, a.gmax, a.thresh, a.cands, a.ncand, a.dump,
+                       a.dump_lo);
     return hipGetLastError();
 }
 
-template <int MODE>
-static hipError_t dispatch(const Launch& l, const ScanArgs& a) {
-    if (l.C2) {
-        switch (l.J) {
-            case 0: return go<0, true, false, MODE>(l, a);
-            case 1: return go<1, true, false, MODE>(l, a);
-            default: return hipErrorInvalidValue;
+template <int J, bool C2, bool EX, int MODE>
+static unsigned int occ(int device) {
+    // cached per (variant, device): resident blocks per CU x CUs
+    static unsigned int cache[64] = {0};
+    if (device < 0 || device >= 64) return 0;
+    if (!cache[device]) {
+        int nb = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kfn<J, C2, EX, MODE>(), 256, 0) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+            return 0;
+        cache[device] = (unsigned int)(nb > 0 ? nb : 1) * (unsigned int)cus;
+    }
+    return cache[device];
+}
+
+// Expands a runtime (J, C2, EX) into the matching template instance and applies F.
+template <int MODE, class F>
+static auto with_variant(int J, int C2, int EX, F&& f) {
+    if (C2) {
+        switch (J) {
+            case 0: return f.template operator()<0, true, false, MODE>();
+            default: return f.template operator()<1, true, false, MODE>();
         }
     }
-    if (l.EX) {
-        switch (l.J) {
-            case 13: return go<13, false, true, MODE>(l, a);
-            case 14: return go<14, false, true, MODE>(l, a);
-            case 15: return go<15, false, true, MODE>(l, a);
-            default: return hipErrorInvalidValue;
+    if (EX) {
+        switch (J) {
+            case 13: return f.template operator()<13, false, true, MODE>();
+            case 14: return f.template operator()<14, false, true, MODE>();
+            default: return f.template operator()<15, false, true, MODE>();
         }
     }
-    switch (l.J) {
-        case 0: return go<0, false, false, MODE>(l, a);
-        case 1: return go<1, false, false, MODE>(l, a);
-        case 2: return go<2, false, false, MODE>(l, a);
-        case 3: return go<3, false, false, MODE>(l, a);
-        case 4: return go<4, false, false, MODE>(l, a);
-        case 5: return go<5, false, false, MODE>(l, a);
-        case 6: return go<6, false, false, MODE>(l, a);
-        case 7: return go<7, false, false, MODE>(l, a);
-        case 8: return go<8, false, false, MODE>(l, a);
-        case 9: return go<9, false, false, MODE>(l, a);
-        case 10: return go<10, false, false, MODE>(l, a);
-        case 11: return go<11, false, false, MODE>(l, a);
-        case 12: return go<12, false, false, MODE>(l, a);
-        case 13: return go<13, false, false, MODE>(l, a);
-        case 14: return go<14, false, false, MODE>(l, a);
-        case 15: return go<15, false, false, MODE>(l, a);
-        default: return hipErrorInvalidValue;
+    switch (J) {
+        case 0: return f.template operator()<0, false, false, MODE>();
+        case 1: return f.template operator()<1, false, false, MODE>();
+        case 2: return f.template operator()<2, false, false, MODE>();
+        case 3: return f.template operator()<3, false, false, MODE>();
+        case 4: return f.template operator()<4, false, false, MODE>();
+        case 5: return f.template operator()<5, false, false, MODE>();
+        case 6: return f.template operator()<6, false, false, MODE>();
+        case 7: return f.template operator()<7, false, false, MODE>();
+        case 8: return f.template operator()<8, false, false, MODE>();
+        case 9: return f.template operator()<9, false, false, MODE>();
+        case 10: return f.template operator()<10, false, false, MODE>();
+        case 11: return f.template operator()<11, false, false, MODE>();
+        case 12: return f.template operator()<12, false, false, MODE>();
+        default: return f.template operator()<13, false, false, MODE>();
     }
 }
 
-hipError_t launch_scan(const Launch& l, int mode, const ScanArgs& a) {
-    return mode == 0 ? dispatch<0>(l, a) : dispatch<1>(l, a);
+static bool valid_variant(int J, int C2, int EX) {
+    if (C2) return !EX && (J == 0 || J == 1);
+    if (EX) return J >= 13 && J <= 15;
+    return J >= 0 && J <= 13;  // J = 14, 15 always need the extra block
+}
+
+struct Launcher {
+    const ScanArgs& a;
+    template <int J, bool C2, bool EX, int MODE>
+    hipError_t operator()() const { return go<J, C2, EX, MODE>(a); }
+};
+
+struct Occupancy {
+    int device;
+    template <int J, bool C2, bool EX, int MODE>
+    unsigned int operator()() const { return occ<J, C2, EX, MODE>(device); }
+};
+
+unsigned int grid_for(int J, int C2, int EX, int mode, int device) {
+    if (!valid_variant(J, C2, EX)) return 0;
+    return mode == 0 ? with_variant<0>(J, C2, EX, Occupancy{device})
+                     : with_variant<1>(J, C2, EX, Occupancy{device});
+}
+
+hipError_t launch_scan(int J, int C2, int EX, int mode, const ScanArgs& a) {
+    if (!valid_variant(J, C2, EX) || a.grid == 0 || a.ndesc <= 0) return hipErrorInvalidValue;
+    return mode == 0 ? with_variant<0>(J, C2, EX, Launcher{a}) : with_variant<1>(J, C2, EX, Launcher{a});
 }
 
 hipError_t launch_reduce(Cand* cands, unsigned int* ncand, Cand* best, hipStream_t stream) {

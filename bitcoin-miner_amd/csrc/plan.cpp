@@ -202,8 +202,11 @@ void build_launch(const uint8_t* msg, uint64_t m, const GroupLayout& g, uint64_t
     D.loop_shift = (uint32_t)(3 - e % 4) * 8u;
     const uint64_t R = pow10u(q), P = pow10u(s);
     D.R = (uint32_t)R;
+    // r values per work item: ~100 keeps every workgroup short (a few ms at full load)
+    // so a launch's tail is small, and still amortises the per-item setup (lane words,
+    // hoisted schedule terms; for C2 the lane block B-1, ~1.1k ops) to ~1-11 ops/nonce.
     uint32_t rc = rchunk_max ? rchunk_max : 100u;
-    D.rchunk = g.C2 ? (uint32_t)R : (uint32_t)std::min<uint64_t>(R, rc);
+    D.rchunk = (uint32_t)std::min<uint64_t>(R, rc);
     D.nrchunks = (uint32_t)((R + D.rchunk - 1) / D.rchunk);
     D.p_first = (uint32_t)((lo / R) % P);
     D.r_first = (uint32_t)(lo % R);

@@ -117,29 +117,23 @@ __device__ __forceinline__ void expand_full(uint32_t (&w)[64]) {
 
 }  // namespace dev
 
-// MODE: 0 = argmin scan (product), 1 = per-nonce hash dump (parity diagnostics).
+// Running best of one wave (wave-uniform, lives in SGPRs): exact lexicographic
+// (hash, nonce) key and the pruning word T (high word of the best hash seen anywhere).
+struct WaveBest {
+    unsigned long long h, n;
+    uint32_t T;
+};
+
+// One row of one launch: 256 consecutive lane values p (row) x loop values [r0, r1).
 template <int J, bool C2, bool EX, int MODE>
-__global__ __launch_bounds__(256) void k_scan(const LaunchDesc D,
-                                              unsigned long long* __restrict__ thresh,
-                                              Cand* __restrict__ cands,
-                                              unsigned int* __restrict__ ncand,
-                                              unsigned long long* __restrict__ dump,
-                                              unsigned long long dump_lo) {
+__device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint32_t r0, uint32_t r1,
+                                         WaveBest& wb, unsigned long long* __restrict__ dump,
+                                         unsigned long long dump_lo) {
     using namespace dev;
-    static_assert(J >= 0 && J < 16, "loop word index");
-    static_assert(!C2 || J <= 1, "C2 layouts have the loop word at J <= 1");
-    static_assert(!EX || J >= 13, "extra padding block only when the last digit is at byte >= 55");
     constexpr DepTable<J> kDep{};
+    const uint32_t p = D.p_first + row * 256u + threadIdx.x;
 
-    const uint32_t tid = threadIdx.x;
-    const uint32_t item = blockIdx.x;
-    const uint32_t pblk = item / D.nrchunks;
-    const uint32_t rc = item - pblk * D.nrchunks;
-    const uint32_t p = D.p_first + pblk * 256u + tid;
-    const uint32_t r_begin = rc * D.rchunk;
-    const uint32_t r_end = min(r_begin + D.rchunk, D.R);
-
-    // ---- per work item: lane words and everything that does not read W_J ----
+    // ---- once per row: lane words and everything that does not read W_J ----
     const uint32_t alo = ascii4(p % 10000u);
     const uint32_t ahi = ascii4((p / 10000u) % 10000u);
     uint32_t W[16];
@@ -183,18 +177,13 @@ __global__ __launch_bounds__(256) void k_scan(const LaunchDesc D,
         }
     }
 
-    // Edge handling: only the first / last lane of the launch has a partial r range,
-    // and lanes past p_last are idle.  Checked only in the (rare) slow path.
+    // Edge handling: only the first / last lane of a launch has a partial r range, and
+    // lanes past p_last are idle.  Checked only in the (rare) slow path.
     const bool lane_ok = p <= D.p_last;
     const uint32_t rlo = (p == D.p_first) ? D.r_first : 0u;
     const uint32_t rhi = (p == D.p_last) ? D.r_last : D.R - 1u;
 
-    unsigned long long tv = 0;
-    if constexpr (MODE == 0) tv = __hip_atomic_load(thresh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t T = __builtin_amdgcn_readfirstlane((uint32_t)(tv >> 32));
-    unsigned long long best_h = ~0ull, best_n = ~0ull;
-
-    for (uint32_t r = r_begin; r < r_end; r++) {
+    for (uint32_t r = r0; r < r1; r++) {
         const uint32_t WJ = D.U[J] | ((ascii4(r) & D.qmask) << D.loop_shift);
         uint32_t w[64];
 #pragma unroll
@@ -243,16 +232,22 @@ __global__ __launch_bounds__(256) void k_scan(const LaunchDesc D,
             H1 = y1 + y.a;
         }
 
+#ifdef GPUHASH_TIE_TEST_BITS
+        // Test-only build (libgpuhash_tietest.so): keep only the top bits of the hash so
+        // equal keys are common and every reduction level's lowest-nonce rule is exercised.
+        H0 >>= (32 - GPUHASH_TIE_TEST_BITS);
+        H1 = 0;
+#endif
         if constexpr (MODE == 1) {
             if (lane_ok && r >= rlo && r <= rhi) {
                 unsigned long long n = D.base + (unsigned long long)p * D.R + r;
                 dump[n - dump_lo] = ((unsigned long long)H0 << 32) | H1;
             }
         } else {
-            unsigned long long m = __builtin_amdgcn_ballot_w64(H0 <= T);
+            unsigned long long m = __builtin_amdgcn_ballot_w64(H0 <= wb.T);
             if (m) {  // wave-uniform, rare once T has settled
                 const bool ok = lane_ok && r >= rlo && r <= rhi;
-                m = __builtin_amdgcn_ballot_w64(H0 <= T && ok);
+                m = __builtin_amdgcn_ballot_w64(H0 <= wb.T && ok);
                 while (m) {
                     const int l = __builtin_ctzll(m);
                     m &= m - 1;
@@ -261,26 +256,96 @@ __global__ __launch_bounds__(256) void k_scan(const LaunchDesc D,
                     const uint32_t pl = __builtin_amdgcn_readlane(p, l);
                     const unsigned long long hh = ((unsigned long long)h0 << 32) | h1;
                     const unsigned long long nn = D.base + (unsigned long long)pl * D.R + r;
-                    if (hh < best_h || (hh == best_h && nn < best_n)) {
-                        best_h = hh;
-                        best_n = nn;
-                        T = h0 < T ? h0 : T;
+                    if (hh < wb.h || (hh == wb.h && nn < wb.n)) {
+                        wb.h = hh;
+                        wb.n = nn;
+                        wb.T = h0 < wb.T ? h0 : wb.T;
                     }
                 }
             }
         }
     }
+}
+
+__device__ __forceinline__ unsigned long long uniform64(unsigned long long v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+// Persistent scan over every launch descriptor of one kernel variant.
+//
+// Work = rows x loop values, linearised in "row-iterations" (one r value for a whole
+// 256-lane row): descriptor i owns [offs[i], offs[i+1]).  Workgroups (a grid sized to
+// the resident capacity) grab contiguous pieces with one atomicAdd -- guided
+// self-scheduling: piece = clamp(remaining / (2 * grid), gmin, gmax) -- so early pieces
+// amortise the per-row setup and the last ones are short, which keeps the tail of the
+// launch to ~gmin iterations.  The wave-uniform best (and its pruning word) persists
+// across pieces; each workgroup appends one 16-byte candidate at the end if it found one.
+template <int J, bool C2, bool EX, int MODE>
+__global__ __launch_bounds__(256) void k_scan(const LaunchDesc* __restrict__ descs,
+                                              const unsigned long long* __restrict__ offs,
+                                              int ndesc, unsigned long long* __restrict__ work,
+                                              unsigned int gmin, unsigned int gmax,
+                                              unsigned long long* __restrict__ thresh,
+                                              Cand* __restrict__ cands,
+                                              unsigned int* __restrict__ ncand,
+                                              unsigned long long* __restrict__ dump,
+                                              unsigned long long dump_lo) {
+    static_assert(J >= 0 && J < 16, "loop word index");
+    static_assert(!C2 || J <= 1, "C2 layouts have the loop word at J <= 1");
+    static_assert(!EX || J >= 13, "extra padding block only when the last digit is at byte >= 55");
+    __shared__ unsigned long long sh_grab[2];
+    __shared__ unsigned long long sh_best[4][2];
+    const uint32_t tid = threadIdx.x;
+    const unsigned long long total = offs[ndesc];
+
+    WaveBest wb{~0ull, ~0ull, 0xFFFFFFFFu};
+    for (;;) {
+        if (tid == 0) {
+            const unsigned long long cur = __hip_atomic_load(work, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long rem = cur < total ? total - cur : 0ull;
+            unsigned long long g = rem / (2ull * gridDim.x);
+            g = g < gmin ? gmin : (g > gmax ? gmax : g);
+            sh_grab[0] = atomicAdd(work, g);
+            sh_grab[1] = g;
+        }
+        __syncthreads();
+        unsigned long long x = uniform64(sh_grab[0]);
+        const unsigned long long g = uniform64(sh_grab[1]);
+        __syncthreads();
+        if (x >= total) break;
+        const unsigned long long end = x + g < total ? x + g : total;
+        if constexpr (MODE == 0) {
+            const unsigned long long tv = __hip_atomic_load(thresh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t t = __builtin_amdgcn_readfirstlane((uint32_t)(tv >> 32));
+            wb.T = t < wb.T ? t : wb.T;
+        }
+        while (x < end) {
+            int i = 0;
+            while (i + 1 < ndesc && offs[i + 1] <= x) i++;
+            const LaunchDesc& D = descs[i];
+            const uint32_t rel = (uint32_t)(x - offs[i]);  // < rows * R <= 2^32 (plan.h)
+            const uint32_t row = rel / D.R, r0 = rel - row * D.R;
+            const unsigned long long left = end - x;
+            const uint32_t r1 = (unsigned long long)(D.R - r0) < left ? D.R : r0 + (uint32_t)left;
+            scan_row<J, C2, EX, MODE>(D, row, r0, r1, wb, dump, dump_lo);
+            x += r1 - r0;
+        }
+    }
 
     if constexpr (MODE == 0) {
-        __shared__ unsigned long long sh[4][2];
         const uint32_t wave = tid >> 6;
-        if ((tid & 63u) == 0) { sh[wave][0] = best_h; sh[wave][1] = best_n; }
+        if ((tid & 63u) == 0) { sh_best[wave][0] = wb.h; sh_best[wave][1] = wb.n; }
         __syncthreads();
         if (tid == 0) {
-            unsigned long long bh = sh[0][0], bn = sh[0][1];
+            unsigned long long bh = sh_best[0][0], bn = sh_best[0][1];
 #pragma unroll
             for (int i = 1; i < 4; i++) {
-                if (sh[i][0] < bh || (sh[i][0] == bh && sh[i][1] < bn)) { bh = sh[i][0]; bn = sh[i][1]; }
+                if (sh_best[i][0] < bh || (sh_best[i][0] == bh && sh_best[i][1] < bn)) {
+                    bh = sh_best[i][0];
+                    bn = sh_best[i][1];
+                }
             }
             if (bh != ~0ull || bn != ~0ull) {
                 atomicMin(thresh, bh);

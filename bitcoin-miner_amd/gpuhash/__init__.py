@@ -25,6 +25,8 @@ from dataclasses import dataclass
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libgpuhash.so")
+# test-only build of the same sources with the hash truncated to 4 bits (ties everywhere)
+TIETEST_LIB_PATH = os.path.join(PKG_DIR, "lib", "libgpuhash_tietest.so")
 
 GPUHASH_OK = 0
 GPUHASH_EINVAL = -1
@@ -120,8 +122,8 @@ def _bytes(msg) -> bytes:
 class Engine:
     """One gpuhash context (one or more gfx950 devices)."""
 
-    def __init__(self, devices: list[int] | None = None):
-        lib = _lib()
+    def __init__(self, devices: list[int] | None = None, lib_path: str | None = None):
+        lib = self._lib = _lib(lib_path)
         ctx = ctypes.c_void_p()
         if devices:
             arr = (ctypes.c_int * len(devices))(*devices)
@@ -134,13 +136,13 @@ class Engine:
 
     @property
     def ndevices(self) -> int:
-        return _lib().gpuhash_ndevices(self._ctx)
+        return self._lib.gpuhash_ndevices(self._ctx)
 
     def min(self, msg, lower: int, upper: int, rchunk: int = 0) -> tuple[int, int]:
         """argmin over inclusive [lower, upper] of (Hash(msg, n), n)."""
         m = _bytes(msg)
         h, n = ctypes.c_uint64(), ctypes.c_uint64()
-        rc = _lib().gpuhash_min_ex(self._ctx, m, len(m), lower, upper, rchunk,
+        rc = self._lib.gpuhash_min_ex(self._ctx, m, len(m), lower, upper, rchunk,
                                    ctypes.byref(h), ctypes.byref(n))
         if rc != GPUHASH_OK:
             raise GpuHashError(rc, "gpuhash_min")
@@ -151,26 +153,26 @@ class Engine:
         import numpy as np
         m = _bytes(msg)
         out = np.empty(count, dtype=np.uint64)
-        rc = _lib().gpuhash_hash_range(self._ctx, m, len(m), lower, count, out.ctypes.data)
+        rc = self._lib.gpuhash_hash_range(self._ctx, m, len(m), lower, count, out.ctypes.data)
         if rc != GPUHASH_OK:
             raise GpuHashError(rc, "gpuhash_hash_range")
         return out
 
     def stats(self) -> dict:
         s = Stats()
-        _lib().gpuhash_last_stats(self._ctx, ctypes.byref(s))
+        self._lib.gpuhash_last_stats(self._ctx, ctypes.byref(s))
         return s.as_dict()
 
     def launches(self) -> list[dict]:
         """Per-launch records (variant, nonces, HIP-event ms) of the last call."""
-        n = _lib().gpuhash_last_launches(self._ctx, None, 0)
+        n = self._lib.gpuhash_last_launches(self._ctx, None, 0)
         arr = (LaunchRecord * max(n, 1))()
-        n = _lib().gpuhash_last_launches(self._ctx, arr, n)
+        n = self._lib.gpuhash_last_launches(self._ctx, arr, n)
         return [arr[i].as_dict() for i in range(n)]
 
     def close(self) -> None:
         if getattr(self, "_ctx", None):
-            _lib().gpuhash_close(self._ctx)
+            self._lib.gpuhash_close(self._ctx)
             self._ctx = None
 
     def __enter__(self):

@@ -116,7 +116,7 @@ def test_rchunk_override(hc, oracle):
     m = b"bradfitz"
     for rc in (1, 7, 10, 33, 1000):
         for i, l in enumerate(plan(hc, m, 123456789, 123499999, rc)):
-            assert l.rchunk == (l.R if l.C2 else min(rc, l.R))
+            assert l.rchunk == min(rc, l.R)
             assert desc_hash(hc, m, 123456789, 123499999, i, l.hi, rc) == oracle.hash(m, l.hi)
 
 
