@@ -71,6 +71,29 @@ def cpu_baseline(seconds: float = 12.0) -> dict:
                       f"{dt:.1f} s; reference Go miner unavailable (no Go toolchain)"}
 
 
+def cpu_baseline_multicore(seconds: float = 5.0) -> dict:
+    """The same loop over contiguous per-thread sub-ranges (the SURVEY's 'one goroutine
+    per core' variant), threads = this process's CPU share capped at 16."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import hash_oracle as ho
+    c = ho.load_c_oracle()
+    try:
+        threads = min(16, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        threads = min(16, os.cpu_count() or 1)
+    n = 1 << 18
+    t = time.perf_counter()
+    c.min(MSG, PER_GPU - n, PER_GPU - 1, threads=threads)
+    dt = time.perf_counter() - t
+    n = max(n, int(n * seconds / max(dt, 1e-6)))
+    lo = PER_GPU - n
+    t = time.perf_counter()
+    c.min(MSG, lo, PER_GPU - 1, threads=threads)
+    dt = time.perf_counter() - t
+    return {"value": n / dt / 1e9, "unit": "GH/s", "cores": threads, "kind": "port",
+            "sample": f"oracle_min_mt over bradfitz [{lo}, {PER_GPU - 1}] ({n} nonces), {dt:.1f} s"}
+
+
 def pmc_traffic(key) -> float | None:
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC
     summary (profiles/pmc_traffic.json: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE,
@@ -90,7 +113,7 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--config", default="2", choices=sorted(CONFIGS))
     args = ap.parse_args()
 
@@ -99,18 +122,27 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
+    # one process per GPU; GPUHASH_DIST_BACKEND=gloo lets several ranks share one GPU
+    # (rehearsing the N>1 path on a 1-GPU box), nccl (= RCCL) is the default
+    backend = os.environ.get("GPUHASH_DIST_BACKEND", "nccl")
+    ndev = max(torch.cuda.device_count(), 1)
+    local = local % ndev
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     import gpuhash
-    from gpuhash.dist import gather_results, merge_min, weak_range
+    from gpuhash.dist import gather_results, merge_min
     eng = gpuhash.Engine([local])
     cfg = CONFIGS[args.config]
     msg, windows = cfg["msg"], cfg["windows"](rank)
     per_gpu = sum(hi - lo + 1 for lo, hi in windows)
     dev = torch.device("cuda", local)
+    coll_dev = dev if backend == "nccl" else None  # gloo gathers CPU tensors
 
     def step(recs=None):
         parts = []
@@ -120,7 +152,7 @@ def main() -> None:
                 recs.extend(eng.launches())  # HIP-event time of every scan launch
         res = merge_min(parts)
         if dist is not None:
-            res = merge_min(gather_results(res, dev))
+            res = merge_min(gather_results(res, coll_dev))
         return res
 
     def barrier():
@@ -138,7 +170,7 @@ def main() -> None:
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev or "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
@@ -192,6 +224,7 @@ def main() -> None:
         }
         if world == 1 and not args.no_cpu_baseline and args.config == "2":
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            out["cpu_baseline_multicore"] = cpu_baseline_multicore(args.cpu_seconds / 2)
         print(json.dumps(out), flush=True)
     eng.close()
     if dist is not None:

@@ -27,14 +27,17 @@ for step in "$@"; do
     case $step in
         valu) run valu 120 ./tools/bin/valu_peak 8 50000; run valu1 120 ./tools/bin/valu_peak 1 50000 ;;
         probe) run probe8 300 ./tools/bin/valu_probe 8 20000 ;;
+        listctr) run listctr 120 rocprofv3 -L ;;
         go) { command -v go && go version; } > "$OUT/go.log" 2>&1; echo "go: $(cat $OUT/go.log)" ;;
         test) run pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
         smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 300 python -u bench.py --steps 10 --warmup 2 ;;
+        dist2) run dist2 300 env GPUHASH_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 ;;
         bench3) run bench3 300 python -u bench.py --config 3 --steps 5 --warmup 1 ;;
         bench4) run bench4 300 python -u bench.py --config 4 --steps 2 --warmup 1 ;;
         prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
-        pmc) run pmc_valu 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/pmc1" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
+        pmc) run pmc_valu 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/pmc1" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
+             run pmc_derived 120 rocprofv3 --pmc VALUBusy VALUUtilization -d "$OUT/pmc4" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
              run pmc_hbm 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc2" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
              run pmc_wr 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc3" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
         *) echo "unknown step $step"; exit 2 ;;

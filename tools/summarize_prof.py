@@ -50,7 +50,7 @@ def main():
     traffic = {"source": f"profiles/{tag}_pmc_summary.json", "kernels": {}}
     merged = collections.defaultdict(dict)
     launches = {}
-    for d in ("pmc1", "pmc2", "pmc3"):
+    for d in ("pmc1", "pmc2", "pmc3", "pmc4"):
         v, n = load_pmc(d)
         for k, cs in v.items():
             for c, x in cs.items():
@@ -63,7 +63,12 @@ def main():
             e["hbm_bytes_per_launch"] = hbm
             traffic["kernels"][k.lower()] = {"hbm_bytes_per_launch": hbm}
         if "GRBM_GUI_ACTIVE" in cs and "SQ_INSTS_VALU" in cs:
-            e["valu_wave_instr_per_xcd_cycle"] = cs["SQ_INSTS_VALU"] / (cs["GRBM_GUI_ACTIVE"] / 8.0)
+            cycles = cs["GRBM_GUI_ACTIVE"] / 8.0  # summed over the 8 XCDs
+            e["gpu_cycles_per_launch"] = cycles
+            # lane-instructions per CU per clock (256 CUs, 64 lanes): 64 = VOP3 issue peak
+            e["valu_lane_ops_per_cu_per_clk"] = cs["SQ_INSTS_VALU"] * 64.0 / 256.0 / cycles
+            if "SQ_INSTS_VALU_INT32" in cs:
+                e["int32_valu_fraction"] = cs["SQ_INSTS_VALU_INT32"] / cs["SQ_INSTS_VALU"]
         summary["kernels"][k] = e
     json.dump(summary, open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w"), indent=1)
     json.dump(traffic, open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
