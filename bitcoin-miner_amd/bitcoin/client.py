@@ -1,0 +1,61 @@
+"""Request client -- bitcoin/client/client.go of the reference (stub at :15), written to
+p1.pdf p.14: send [Request message 0 maxNonce], print "Result minHash nonce", or
+"Disconnected" if the server is lost (printResult / printDisconnected, client.go:19-26).
+
+    python bitcoin-miner_amd/bin/client host:port message maxNonce
+"""
+from __future__ import annotations
+
+import sys
+
+import lsp
+
+from . import NewRequest, MsgType, marshal, params_from_env, unmarshal
+
+
+def printResult(hash_: str, nonce: str) -> None:  # client.go:19-21
+    print("Result", hash_, nonce, flush=True)
+
+
+def printDisconnected() -> None:  # client.go:24-26
+    print("Disconnected", flush=True)
+
+
+def request(hostport: str, message: str, max_nonce: int, params=None):
+    """Returns (hash, nonce), or None when the connection to the server is lost."""
+    try:
+        c = lsp.NewClient(hostport, params or params_from_env())
+    except lsp.LSPError:
+        return None
+    try:
+        c.Write(marshal(NewRequest(message, 0, max_nonce)))
+        while True:
+            m = unmarshal(c.Read())
+            if m.Type == MsgType.Result:
+                return m.Hash, m.Nonce
+    except lsp.LSPError:
+        return None
+    finally:
+        c.Close()
+
+
+def main(argv=None) -> int:
+    argv = sys.argv if argv is None else argv
+    if len(argv) != 4:  # client.go:9-13
+        print("Usage: ./client <hostport> <message> <maxNonce>")
+        return 0
+    try:
+        max_nonce = int(argv[3])
+    except ValueError:
+        print(f"{argv[3]} is not a number.")
+        return 0
+    res = request(argv[1], argv[2], max_nonce)
+    if res is None:
+        printDisconnected()
+    else:
+        printResult(str(res[0]), str(res[1]))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

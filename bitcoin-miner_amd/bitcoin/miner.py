@@ -1,0 +1,63 @@
+"""Miner -- bitcoin/miner/miner.go of the reference (stub; "TODO: implement this!" at :15),
+written to p1.pdf pp.13-15 with the min-hash loop replaced by ONE call into the gfx950
+engine (gpuhash_min through the C ABI):
+
+    Join -> loop { Read Request -> gpuhash_min(Data, Lower, Upper) -> Write Result }
+    and shut down when the server is lost (p1.pdf p.15).
+
+    python bitcoin-miner_amd/bin/miner host:port      (GPUHASH_DEVICES=0,1 narrows devices)
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import lsp
+
+from . import MsgType, NewJoin, NewResult, marshal, params_from_env, unmarshal
+
+
+def open_engine():
+    import gpuhash
+    devs = os.environ.get("GPUHASH_DEVICES")
+    return gpuhash.Engine([int(x) for x in devs.split(",")] if devs else None)
+
+
+def run(hostport: str, engine=None, params=None, on_client=None) -> int:
+    """Serves jobs until the server is lost.  `engine` is anything with
+    .min(msg, lower, upper) -> (hash, nonce); by default the gpuhash Engine.
+    `on_client` (tests) receives the LSP client once connected."""
+    try:
+        c = lsp.NewClient(hostport, params or params_from_env())
+    except lsp.LSPError:
+        return 1
+    if on_client is not None:
+        on_client(c)
+    engine = engine or open_engine()
+    jobs = 0
+    try:
+        c.Write(marshal(NewJoin()))
+        while True:
+            m = unmarshal(c.Read())
+            if m.Type != MsgType.Request:
+                continue
+            # was: for n := m.Lower; n <= m.Upper; n++ { h := bitcoin.Hash(m.Data, n) ... }
+            h, n = engine.min(m.Data, m.Lower, m.Upper)
+            c.Write(marshal(NewResult(h, n)))
+            jobs += 1
+    except lsp.LSPError:
+        return 0  # server lost: shut down (p1.pdf p.15)
+    finally:
+        c.Close()
+
+
+def main(argv=None) -> int:
+    argv = sys.argv if argv is None else argv
+    if len(argv) != 2:  # miner.go:9-13
+        print("Usage: ./miner <hostport>")
+        return 0
+    return run(argv[1])
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,198 @@
+"""Server -- bitcoin/server/server.go of the reference (stub at :15), written to p1.pdf
+pp.13-15: split each client Request into jobs, farm them to miners, merge the Results,
+answer the client.
+
+Job chunking: the reference leaves "a suitable maximum job size"
+open.  With GPU miners at ~34 GH/s each, a job of 2^34 nonces is ~0.5 s of GPU time:
+big enough that per-job overhead (one LSP round trip + one gpuhash_min call, ~ms) is
+<1%, small enough that a killed miner loses half a second of work and 16 concurrent
+requests still spread over 8 miners.  GPUHASH_JOB_SIZE overrides it.
+
+Scheduler (p1.pdf p.15, "balances loads across all requests"): an idle miner always
+gets the next job of the outstanding request that currently has the FEWEST jobs in
+flight (ties: oldest request first), so the workers assigned to each request differ by
+at most one whenever requests have work queued.
+
+Failures (p1.pdf p.15): a lost miner's job goes back to the FRONT of its request's queue
+(and waits for a miner if none is left); a lost client's requests are dropped -- queued
+jobs are discarded, in-flight results are ignored when they arrive.
+
+Merging: results fold with the lexicographic (hash, nonce) key, so the answer is the
+same however the range is chunked (lowest nonce among equal hashes).
+
+    python bitcoin-miner_amd/bin/server port
+"""
+from __future__ import annotations
+
+import collections
+import itertools
+import os
+import sys
+from dataclasses import dataclass, field
+
+import lsp
+
+from . import MsgType, NewRequest, NewResult, marshal, params_from_env, unmarshal
+
+DEFAULT_JOB_SIZE = 1 << 34
+
+
+@dataclass
+class Job:
+    req_id: int
+    lower: int
+    upper: int
+
+
+@dataclass
+class Request:
+    req_id: int
+    client: int
+    data: str
+    pending: collections.deque = field(default_factory=collections.deque)
+    inflight: int = 0
+    best: tuple | None = None
+
+
+def split_jobs(req_id: int, lower: int, upper: int, size: int):
+    """Contiguous jobs of at most `size` nonces covering the inclusive range."""
+    lo = lower
+    while True:
+        hi = min(upper, lo + size - 1)
+        yield Job(req_id, lo, hi)
+        if hi >= upper:
+            return
+        lo = hi + 1
+
+
+class Scheduler:
+    """Pure bookkeeping (no I/O): tests drive it directly."""
+
+    def __init__(self, job_size: int = DEFAULT_JOB_SIZE):
+        self.job_size = job_size
+        self.requests: dict[int, Request] = {}
+        self.miners: dict[int, Job | None] = {}   # miner conn -> job in flight
+        self.idle: collections.deque = collections.deque()
+        self._ids = itertools.count(1)
+
+    def add_miner(self, conn: int) -> None:
+        if conn not in self.miners:
+            self.miners[conn] = None
+            self.idle.append(conn)
+
+    def add_request(self, client: int, data: str, lower: int, upper: int) -> int:
+        rid = next(self._ids)
+        r = Request(rid, client, data)
+        if lower <= upper:
+            r.pending.extend(split_jobs(rid, lower, upper, self.job_size))
+        self.requests[rid] = r
+        return rid
+
+    def next_assignment(self):
+        """(miner, job, data) for the next dispatch, or None."""
+        while self.idle:
+            cands = [r for r in self.requests.values() if r.pending]
+            if not cands:
+                return None
+            r = min(cands, key=lambda x: (x.inflight, x.req_id))
+            miner = self.idle.popleft()
+            if miner not in self.miners:
+                continue
+            job = r.pending.popleft()
+            r.inflight += 1
+            self.miners[miner] = job
+            return miner, job, r.data
+        return None
+
+    def result(self, miner: int, h: int, n: int):
+        """Folds a miner's result; returns (client, (hash, nonce)) when a request is done."""
+        job = self.miners.get(miner)
+        if job is None:
+            return None
+        self.miners[miner] = None
+        self.idle.append(miner)
+        r = self.requests.get(job.req_id)
+        if r is None:  # the client is gone: ignore the result
+            return None
+        r.inflight -= 1
+        if r.best is None or (h, n) < r.best:
+            r.best = (h, n)
+        if not r.pending and r.inflight == 0:
+            del self.requests[r.req_id]
+            return r.client, r.best
+        return None
+
+    def lost(self, conn: int) -> None:
+        if conn in self.miners:
+            job = self.miners.pop(conn)
+            try:
+                self.idle.remove(conn)
+            except ValueError:
+                pass
+            if job is not None and job.req_id in self.requests:
+                r = self.requests[job.req_id]
+                r.inflight -= 1
+                r.pending.appendleft(job)
+        for rid in [rid for rid, r in self.requests.items() if r.client == conn]:
+            del self.requests[rid]
+
+
+def serve(port: int, params=None, job_size: int | None = None, ready=None, log=None) -> None:
+    """Runs the server until its LSP server is closed."""
+    srv = lsp.NewServer(port, params or params_from_env())
+    if ready is not None:
+        ready(srv)
+    sched = Scheduler(job_size or int(os.environ.get("GPUHASH_JOB_SIZE", DEFAULT_JOB_SIZE)))
+
+    def dispatch():
+        while True:
+            a = sched.next_assignment()
+            if a is None:
+                return
+            miner, job, data = a
+            try:
+                srv.Write(miner, marshal(NewRequest(data, job.lower, job.upper)))
+            except lsp.LSPError:
+                sched.lost(miner)
+
+    while True:
+        try:
+            conn, payload = srv.Read()
+        except lsp.LSPError as e:
+            if e.conn_id == 0:
+                return  # server closed
+            sched.lost(e.conn_id)
+            dispatch()
+            continue
+        try:
+            m = unmarshal(payload)
+        except (ValueError, KeyError):
+            continue
+        if m.Type == MsgType.Join:
+            sched.add_miner(conn)
+        elif m.Type == MsgType.Request:
+            sched.add_request(conn, m.Data, m.Lower, m.Upper)
+        elif m.Type == MsgType.Result:
+            done = sched.result(conn, m.Hash, m.Nonce)
+            if done is not None:
+                client, (h, n) = done
+                try:
+                    srv.Write(client, marshal(NewResult(h, n)))
+                except lsp.LSPError:
+                    pass
+        if log:
+            log(m, sched)
+        dispatch()
+
+
+def main(argv=None) -> int:
+    argv = sys.argv if argv is None else argv
+    if len(argv) != 2:  # server.go:9-13
+        print("Usage: ./server <port>")
+        return 0
+    serve(int(argv[1]))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

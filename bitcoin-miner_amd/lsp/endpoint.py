@@ -1,0 +1,174 @@
+"""Per-connection LSP state machine + the single-threaded event loop both sides use.
+
+Protocol (p1.pdf pp.2-7; the reference's attempt is lsp/client_impl.go and
+lsp/server_impl.go, which cannot carry data as written -- SURVEY.md 2 rows 8-9):
+  * data messages carry per-direction sequence numbers from 1 and are each acked;
+  * sliding window: with n the oldest unacknowledged seq, only n..n+w-1 may be sent;
+  * the receiver delivers in order, acks duplicates again, and remembers the last w
+    distinct data messages it received;
+  * every epoch: resend unacked data, re-ack the last w received messages, send Ack 0
+    if no data has been received yet (heartbeat / connect ack), and count the epoch as
+    silent unless something arrived; K silent epochs => connection lost.
+
+Like the reference's design (one handleMessages goroutine per endpoint), one loop
+thread owns all protocol state; API calls post commands to it through a queue.
+"""
+from __future__ import annotations
+
+import collections
+import queue
+import selectors
+import socket
+import threading
+import time
+
+from .message import Message, MsgType, NewAck, NewData
+
+
+class ConnState:
+    """One side of one connection."""
+
+    def __init__(self, conn_id: int, window: int, epoch_limit: int, send):
+        self.conn_id = conn_id
+        self.w = max(1, window)
+        self.k = max(1, epoch_limit)
+        self.send = send                     # send(Message)
+        self.next_seq = 1                    # next data seq to assign
+        self.pending = collections.deque()   # (seq, payload) not yet inside the window
+        self.unacked = {}                    # seq -> payload, sent and not acked
+        self.expected = 1                    # next seq to deliver
+        self.rbuf = {}                       # received out of order
+        self.recent = collections.deque(maxlen=self.w)  # last w distinct received seqs
+        self.got_data = False
+        self.silent = 0
+        self.lost = False
+        self.closing = False
+
+    # -- sending ---------------------------------------------------------------
+    def window_base(self) -> int:
+        if self.unacked:
+            return min(self.unacked)
+        if self.pending:
+            return self.pending[0][0]
+        return self.next_seq
+
+    def pump(self) -> None:
+        base = self.window_base()
+        while self.pending and self.pending[0][0] < base + self.w:
+            seq, payload = self.pending.popleft()
+            self.unacked[seq] = payload
+            self.send(NewData(self.conn_id, seq, payload))
+
+    def write(self, payload: bytes) -> None:
+        self.pending.append((self.next_seq, payload))
+        self.next_seq += 1
+        self.pump()
+
+    def flushed(self) -> bool:
+        return not self.pending and not self.unacked
+
+    # -- receiving -------------------------------------------------------------
+    def on_message(self, m: Message) -> list:
+        """Handles one message from the peer; returns payloads now deliverable in order."""
+        self.silent = 0
+        if m.Type == MsgType.MsgAck:
+            if m.SeqNum in self.unacked:
+                del self.unacked[m.SeqNum]
+                self.pump()
+            return []
+        if m.Type != MsgType.MsgData:
+            return []
+        self.send(NewAck(self.conn_id, m.SeqNum))
+        out = []
+        if m.SeqNum >= self.expected and m.SeqNum not in self.rbuf and m.SeqNum < self.expected + self.w:
+            self.rbuf[m.SeqNum] = m.Payload or b""
+            self.recent.append(m.SeqNum)
+            self.got_data = True
+            while self.expected in self.rbuf:
+                out.append(self.rbuf.pop(self.expected))
+                self.expected += 1
+        return out
+
+    # -- epochs ----------------------------------------------------------------
+    def on_epoch(self) -> None:
+        """Epoch actions (p1.pdf p.6).  Marks the connection lost after K silent epochs."""
+        if self.lost:
+            return
+        self.silent += 1
+        if self.silent >= self.k:
+            self.lost = True
+            return
+        if not self.got_data:
+            self.send(NewAck(self.conn_id, 0))
+        for seq in sorted(self.unacked):
+            self.send(NewData(self.conn_id, seq, self.unacked[seq]))
+        for seq in self.recent:
+            self.send(NewAck(self.conn_id, seq))
+
+
+class Loop:
+    """Event loop thread: UDP readiness, a command queue with a wakeup socket, epochs."""
+
+    def __init__(self, conn, epoch_ms: int, on_datagram, on_command, on_epoch):
+        self.conn = conn
+        self.epoch = epoch_ms / 1000.0
+        self.on_datagram, self.on_command, self.on_epoch = on_datagram, on_command, on_epoch
+        self.cmds = queue.Queue()
+        self._r, self._w = socket.socketpair()
+        self._r.setblocking(False)
+        self.stopped = threading.Event()
+        self._stop = False
+        self.thread = threading.Thread(target=self._run, daemon=True)
+
+    def start(self) -> None:
+        self.thread.start()
+
+    def post(self, *cmd) -> None:
+        self.cmds.put(cmd)
+        try:
+            self._w.send(b"x")
+        except OSError:
+            pass
+
+    def stop(self) -> None:
+        self._stop = True
+
+    def _run(self) -> None:
+        sel = selectors.DefaultSelector()
+        sel.register(self.conn.sock, selectors.EVENT_READ, "udp")
+        sel.register(self._r, selectors.EVENT_READ, "wake")
+        next_epoch = time.monotonic() + self.epoch
+        try:
+            while not self._stop:
+                timeout = max(0.0, next_epoch - time.monotonic())
+                for key, _ in sel.select(timeout):
+                    if key.data == "udp":
+                        while True:
+                            try:
+                                got = self.conn.read_from()
+                            except (BlockingIOError, InterruptedError):
+                                break
+                            except OSError:
+                                break
+                            if got is not None:
+                                self.on_datagram(*got)
+                    else:
+                        try:
+                            while self._r.recv(4096):
+                                pass
+                        except (BlockingIOError, InterruptedError):
+                            pass
+                while True:
+                    try:
+                        cmd = self.cmds.get_nowait()
+                    except queue.Empty:
+                        break
+                    self.on_command(cmd)
+                if time.monotonic() >= next_epoch:
+                    next_epoch = time.monotonic() + self.epoch
+                    self.on_epoch()
+        finally:
+            sel.close()
+            self._r.close()
+            self._w.close()
+            self.stopped.set()

@@ -1,0 +1,187 @@
+"""CPU: the LSP transport (bitcoin-miner_amd/lsp) that carries Request/Result messages.
+
+Modelled on the reference's own LSP suite (src/github.com/cmu440/lsp/lsp{1,2,3,4}_test.go):
+an echo server with several clients (lsp1 TestBasic*), write drops (TestRobust*), window
+sizes with scattered/in-order delivery (lsp2 TestWindow*), explicit closes and lost
+connections (lsp3/lsp4).  Epochs are shortened so the suite runs in seconds.
+"""
+import random
+import threading
+import time
+
+import pytest
+
+import lsp
+import lspnet
+
+FAST = dict(EpochLimit=5, EpochMillis=50)
+
+
+@pytest.fixture(autouse=True)
+def no_drops():
+    lspnet.SetReadDropPercent(0)
+    lspnet.SetWriteDropPercent(0)
+    yield
+    lspnet.SetReadDropPercent(0)
+    lspnet.SetWriteDropPercent(0)
+
+
+def echo_server(params):
+    srv = lsp.NewServer(0, params)
+    stop = threading.Event()
+
+    def loop():
+        while not stop.is_set():
+            try:
+                cid, payload = srv.Read()
+            except lsp.LSPError as e:
+                if e.conn_id == 0:
+                    return
+                continue
+            try:
+                srv.Write(cid, payload)
+            except lsp.LSPError:
+                pass
+
+    t = threading.Thread(target=loop, daemon=True)
+    t.start()
+    return srv, stop, t
+
+
+def run_echo(nclients, nmsgs, params, drop=0):
+    srv, stop, t = echo_server(params)
+    clients = [lsp.NewClient(f"127.0.0.1:{srv.port}", params) for _ in range(nclients)]
+    assert len({c.ConnID() for c in clients}) == nclients
+    lspnet.SetWriteDropPercent(drop)
+    errors = []
+
+    def client_loop(c, seed):
+        rng = random.Random(seed)
+        msgs = [str(rng.randrange(10 ** 9)).encode() for _ in range(nmsgs)]
+        for m in msgs:
+            c.Write(m)
+        got = [c.Read() for _ in msgs]
+        if got != msgs:
+            errors.append((c.ConnID(), got[:3], msgs[:3]))
+
+    ts = [threading.Thread(target=client_loop, args=(c, i)) for i, c in enumerate(clients)]
+    for x in ts:
+        x.start()
+    for x in ts:
+        x.join(60)
+    lspnet.SetWriteDropPercent(0)
+    for c in clients:
+        c.Close()
+    stop.set()
+    srv.Close()
+    assert not errors, errors
+
+
+@pytest.mark.parametrize("nclients,nmsgs", [(1, 1), (1, 50), (3, 30), (10, 20)])
+def test_basic_echo(nclients, nmsgs):
+    run_echo(nclients, nmsgs, lsp.Params(WindowSize=1, **FAST))
+
+
+@pytest.mark.parametrize("window", [1, 2, 5, 10])
+def test_window_sizes(window):
+    run_echo(3, 40, lsp.Params(WindowSize=window, **FAST))
+
+
+@pytest.mark.parametrize("drop", [10, 20])
+def test_robust_with_write_drops(drop):
+    run_echo(4, 25, lsp.Params(EpochLimit=20, EpochMillis=20, WindowSize=4), drop=drop)
+
+
+def test_in_order_delivery_under_reordering_window():
+    # a window of 8 lets up to 8 messages be in flight; the receiver must still deliver
+    # in sequence-number order (lsp2 "scattered" mode)
+    params = lsp.Params(EpochLimit=20, EpochMillis=20, WindowSize=8)
+    run_echo(2, 100, params, drop=15)
+
+
+def test_json_wire_format_matches_go():
+    m = lsp.NewData(3, 7, b"hello")
+    assert m.marshal() == b'{"Type":1,"ConnID":3,"SeqNum":7,"Payload":"aGVsbG8="}'
+    assert lsp.Message.unmarshal(m.marshal()) == m
+    assert lsp.NewAck(3, 0).marshal() == b'{"Type":2,"ConnID":3,"SeqNum":0,"Payload":null}'
+    assert str(m) == "[Data 3 7 hello]"
+    assert str(lsp.NewParams()) == "[EpochLimit: 5, EpochMillis: 2000, WindowSize: 1]"
+
+
+def test_connect_fails_without_server():
+    t = time.time()
+    with pytest.raises(lsp.LSPError):
+        lsp.NewClient("127.0.0.1:9", lsp.Params(EpochLimit=3, EpochMillis=30))
+    assert time.time() - t < 5
+
+
+def test_client_detects_lost_server():
+    params = lsp.Params(**FAST)
+    srv = lsp.NewServer(0, params)
+    c = lsp.NewClient(f"127.0.0.1:{srv.port}", params)
+    srv.Close()  # no clients pending -> returns; the client now hears nothing
+    t = time.time()
+    with pytest.raises(lsp.LSPError):
+        c.Read()
+    assert time.time() - t < 2
+    with pytest.raises(lsp.LSPError):
+        c.Write(b"x")
+    c.Close()
+
+
+def test_server_detects_lost_client_and_reports_conn_id():
+    params = lsp.Params(**FAST)
+    srv = lsp.NewServer(0, params)
+    c = lsp.NewClient(f"127.0.0.1:{srv.port}", params)
+    c.Write(b"hi")
+    assert srv.Read() == (c.ConnID(), b"hi")
+    c._loop.stop()  # kill the client without a Close: it goes silent
+    with pytest.raises(lsp.LSPError) as e:
+        srv.Read()
+    assert e.value.conn_id == c.ConnID()
+    with pytest.raises(lsp.LSPError):
+        srv.Write(c.ConnID(), b"late")
+    srv.Close()
+
+
+def test_close_conn_flushes_pending_then_reports():
+    params = lsp.Params(WindowSize=2, **FAST)
+    srv = lsp.NewServer(0, params)
+    c = lsp.NewClient(f"127.0.0.1:{srv.port}", params)
+    c.Write(b"hello")
+    cid, _ = srv.Read()
+    for i in range(5):
+        srv.Write(cid, b"m%d" % i)
+    srv.CloseConn(cid)
+    assert [c.Read() for _ in range(5)] == [b"m%d" % i for i in range(5)]
+    with pytest.raises(lsp.LSPError) as e:
+        srv.Read()
+    assert e.value.conn_id == cid
+    c.Close()
+    srv.Close()
+
+
+def test_client_close_waits_for_acks():
+    params = lsp.Params(EpochLimit=20, EpochMillis=20, WindowSize=1)
+    srv = lsp.NewServer(0, params)
+    c = lsp.NewClient(f"127.0.0.1:{srv.port}", params)
+    lspnet.SetClientWriteDropPercent(30)
+    for i in range(20):
+        c.Write(b"%d" % i)
+    c.Close()  # returns only when all 20 are acknowledged
+    lspnet.SetClientWriteDropPercent(0)
+    got = [srv.Read()[1] for _ in range(20)]
+    assert got == [b"%d" % i for i in range(20)]
+    srv.Close()
+
+
+def test_duplicate_connect_same_address_keeps_one_connection():
+    params = lsp.Params(**FAST)
+    srv = lsp.NewServer(0, params)
+    c = lsp.NewClient(f"127.0.0.1:{srv.port}", params)
+    for _ in range(3):
+        c._conn.write_to(lsp.NewConnect().marshal())
+    time.sleep(0.1)
+    assert len(srv._conns) == 1
+    c.Close()
+    srv.Close()
