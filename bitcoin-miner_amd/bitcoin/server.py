@@ -122,24 +122,36 @@ class Scheduler:
             return r.client, r.best
         return None
 
-    def lost(self, conn: int) -> None:
+    def lost(self, conn: int) -> str | None:
+        """Forgets a lost connection; returns a log line describing what changed."""
+        note = None
         if conn in self.miners:
             job = self.miners.pop(conn)
             try:
                 self.idle.remove(conn)
             except ValueError:
                 pass
+            note = f"miner {conn} lost"
             if job is not None and job.req_id in self.requests:
                 r = self.requests[job.req_id]
                 r.inflight -= 1
                 r.pending.appendleft(job)
-        for rid in [rid for rid, r in self.requests.items() if r.client == conn]:
+                note += f"; job [{job.lower}, {job.upper}] of request {job.req_id} requeued"
+        dropped = [rid for rid, r in self.requests.items() if r.client == conn]
+        for rid in dropped:
             del self.requests[rid]
+        if dropped:
+            note = f"client {conn} lost; dropped request(s) {dropped}"
+        return note
 
 
 def serve(port: int, params=None, job_size: int | None = None, ready=None, log=None) -> None:
-    """Runs the server until its LSP server is closed."""
+    """Runs the server until its LSP server is closed.  `log(str)` (or GPUHASH_SERVER_LOG=1
+    for stderr) receives joins, requests and failure handling."""
     srv = lsp.NewServer(port, params or params_from_env())
+    if log is None and os.environ.get("GPUHASH_SERVER_LOG"):
+        def log(line):  # stderr only: stdout of the programs is graded (p1.pdf p.15)
+            print(f"server: {line}", file=sys.stderr, flush=True)
     if ready is not None:
         ready(srv)
     sched = Scheduler(job_size or int(os.environ.get("GPUHASH_JOB_SIZE", DEFAULT_JOB_SIZE)))
@@ -153,7 +165,9 @@ def serve(port: int, params=None, job_size: int | None = None, ready=None, log=N
             try:
                 srv.Write(miner, marshal(NewRequest(data, job.lower, job.upper)))
             except lsp.LSPError:
-                sched.lost(miner)
+                note = sched.lost(miner)
+                if log and note:
+                    log(note)
 
     while True:
         try:
@@ -161,7 +175,9 @@ def serve(port: int, params=None, job_size: int | None = None, ready=None, log=N
         except lsp.LSPError as e:
             if e.conn_id == 0:
                 return  # server closed
-            sched.lost(e.conn_id)
+            note = sched.lost(e.conn_id)
+            if log and note:
+                log(note)
             dispatch()
             continue
         try:
@@ -180,8 +196,8 @@ def serve(port: int, params=None, job_size: int | None = None, ready=None, log=N
                     srv.Write(client, marshal(NewResult(h, n)))
                 except lsp.LSPError:
                     pass
-        if log:
-            log(m, sched)
+        if log and m.Type != MsgType.Result:
+            log(f"conn {conn}: {m}")
         dispatch()
 
 

@@ -87,7 +87,8 @@ def test_config5_scaled_drops_and_killed_miner(procs, engine, oracle):
     port = free_port()
     drops = dict(LSPNET_CLIENT_READ_DROP=10, LSPNET_CLIENT_WRITE_DROP=10,
                  LSPNET_SERVER_READ_DROP=10, LSPNET_SERVER_WRITE_DROP=10)
-    procs.start([os.path.join(BIN, "server"), str(port)], env=env(GPUHASH_JOB_SIZE=1 << 32, **drops))
+    server = procs.start([os.path.join(BIN, "server"), str(port)],
+                         env=env(GPUHASH_JOB_SIZE=1 << 32, GPUHASH_SERVER_LOG=1, **drops))
     time.sleep(0.5)
     miners = [procs.start([os.path.join(BIN, "miner"), f"127.0.0.1:{port}"], env=env(**drops))
               for _ in range(4)]
@@ -105,3 +106,6 @@ def test_config5_scaled_drops_and_killed_miner(procs, engine, oracle):
         msg = f"client-{i:02d}".encode()
         assert (h, n) == engine.min(msg, 0, max_nonce), i
         assert oracle.hash(msg, n) == h
+    server.send_signal(signal.SIGTERM)
+    log = server.communicate(timeout=30)[1]
+    assert "lost; job [" in log and "requeued" in log, log[-2000:]  # the killed miner's job was re-run
