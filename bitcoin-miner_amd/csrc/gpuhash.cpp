@@ -242,10 +242,10 @@ int gpuhash_open(const int* devices, int ndevices, gpuhash_ctx** out) {
     if (ndevices == 0) {
         for (int i = 0; i < count; i++) ords.push_back(i);
     } else {
+        // A device may be listed more than once: each entry gets its own stream and
+        // buffers and takes its own shard (rehearses the multi-device path on one GPU).
         for (int i = 0; i < ndevices; i++) {
             if (devices[i] < 0 || devices[i] >= count) return GPUHASH_EINVAL;
-            for (int o : ords)
-                if (o == devices[i]) return GPUHASH_EINVAL;
             ords.push_back(devices[i]);
         }
     }

@@ -1,4 +1,6 @@
 // kernels.hip -- instantiates the gfx950 scan kernels and the candidate reduce.
+#include <atomic>
+
 #include "kernels.h"
 #include "scan_kernel.h"
 
@@ -54,17 +56,20 @@ static hipError_t go(const ScanArgs& a) {
 
 template <int J, bool C2, bool EX, int MODE>
 static unsigned int occ(int device) {
-    // cached per (variant, device): resident blocks per CU x CUs
-    static unsigned int cache[64] = {0};
+    // cached per (variant, device): resident blocks per CU x CUs.  Device threads may
+    // race to fill an entry; they compute the same value.
+    static std::atomic<unsigned int> cache[64];
     if (device < 0 || device >= 64) return 0;
-    if (!cache[device]) {
+    unsigned int v = cache[device].load(std::memory_order_relaxed);
+    if (!v) {
         int nb = 0, cus = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kfn<J, C2, EX, MODE>(), 256, 0) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
             return 0;
-        cache[device] = (unsigned int)(nb > 0 ? nb : 1) * (unsigned int)cus;
+        v = (unsigned int)(nb > 0 ? nb : 1) * (unsigned int)cus;
+        cache[device].store(v, std::memory_order_relaxed);
     }
-    return cache[device];
+    return v;
 }
 
 // Expands a runtime (J, C2, EX) into the matching template instance and applies F.

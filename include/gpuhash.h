@@ -72,7 +72,8 @@ typedef struct gpuhash_launch_record {
 } gpuhash_launch_record;
 
 /* Opens the listed devices (HIP ordinals); ndevices == 0 means every visible device.
- * Allocates per-device streams, events and a small candidate buffer.
+ * Allocates per-device streams, events and a small candidate buffer.  An ordinal may be
+ * listed more than once (each entry is a separate shard with its own stream).
  * Replaces: nothing in the reference (the miner would call it once at start-up,
  * miner.go:8-16). */
 int gpuhash_open(const int *devices, int ndevices, gpuhash_ctx **out);

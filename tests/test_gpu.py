@@ -121,9 +121,23 @@ def test_errors_are_loud(engine):
         engine.min(b"x", 10, 9)
     assert e.value.rc == gpuhash.GPUHASH_EINVAL
     with pytest.raises(gpuhash.GpuHashError):
-        gpuhash.Engine([0, 0])
+        gpuhash.Engine([0, 99])
     with pytest.raises(gpuhash.GpuHashError):
         engine.hash_range(b"x", U64, 2)  # wraps past 2^64-1
+
+
+def test_multi_device_sharding_and_host_argmin(engine, oracle):
+    """The in-process multi-device path (static cost-balanced shards, one host thread +
+    stream per entry, 16-byte host argmin) run as 3 shards on the one GPU of the box."""
+    import gpuhash
+    with gpuhash.Engine([0, 0, 0]) as multi:
+        assert multi.ndevices == 3
+        for m, lo, hi in [(b"bradfitz", 0, (1 << 32) - 1), (M120, 999_000_000, 1_001_000_000),
+                          (b"x", 5, 7), (b"y" * 50, U64 - 10 ** 7, U64)]:
+            assert multi.min(m, lo, hi) == engine.min(m, lo, hi)
+        st = multi.stats()
+        assert st["ndevices"] == 3 and st["launches"] >= 3
+        assert multi.min(b"bradfitz", 0, 9999) == oracle.min(b"bradfitz", 0, 9999)
 
 
 def test_native_library_is_the_one_loaded(engine):

@@ -73,7 +73,12 @@ def run_echo(nclients, nmsgs, params, drop=0):
     for c in clients:
         c.Close()
     stop.set()
-    srv.Close()
+    try:
+        srv.Close()
+    except lsp.LSPError:
+        # a closed client may never ack the server's last retransmission when its ack
+        # was dropped; Close then reports the lost client (server_api.go:33-38)
+        pass
     assert not errors, errors
 
 

@@ -28,12 +28,14 @@ for step in "$@"; do
         valu) run valu 120 ./tools/bin/valu_peak 8 50000; run valu1 120 ./tools/bin/valu_peak 1 50000 ;;
         probe) run probe8 300 ./tools/bin/valu_probe 8 20000 ;;
         listctr) run listctr 120 rocprofv3 -L ;;
+        clocks) { rocm-smi --showclocks; amd-smi metric --clock 2>&1 | head -40; } > "$OUT/clocks.log" 2>&1; cat "$OUT/clocks.log" | head -30 ;;
         go) { command -v go && go version; } > "$OUT/go.log" 2>&1; echo "go: $(cat $OUT/go.log)" ;;
         test) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
         systest) run pytest_sys 600 python -u -m pytest tests/test_gpu_system.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 300 python -u bench.py --steps 10 --warmup 2 ;;
         dist2) run dist2 300 env GPUHASH_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 ;;
+        sweep) run sweep 600 python -u tools/layout_sweep.py ;;
         sys5) run sys5 900 python -u tools/system_bench.py ;;
         bench3) run bench3 300 python -u bench.py --config 3 --steps 5 --warmup 1 ;;
         bench4) run bench4 300 python -u bench.py --config 4 --steps 2 --warmup 1 ;;
