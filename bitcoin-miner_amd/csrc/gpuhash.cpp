@@ -33,6 +33,9 @@ struct Dev {
     uint8_t* d_meta = nullptr;
     uint8_t* h_meta = nullptr;
     size_t meta_cap = 0;
+    // uniform K+W tables of C2/J=0 descriptors (one per digit count), grow-only
+    uint32_t* d_ktab = nullptr;
+    size_t ktab_cap = 0;  // words
     std::vector<hipEvent_t> ev;
     // per-call results
     int rc = GPUHASH_OK;
@@ -80,6 +83,7 @@ static void dev_free(Dev& d) {
     if (d.d_cands) hipFree(d.d_cands);
     if (d.h_best) hipHostFree(d.h_best);
     if (d.d_meta) hipFree(d.d_meta);
+    if (d.d_ktab) hipFree(d.d_ktab);
     if (d.h_meta) hipHostFree(d.h_meta);
     if (d.stream) hipStreamDestroy(d.stream);
     d = Dev{};
@@ -96,6 +100,16 @@ static int dev_reserve_meta(Dev& d, size_t bytes) {
     if (hipMalloc(&d.d_meta, cap) != hipSuccess) return GPUHASH_ENOMEM;
     if (hipHostMalloc(&d.h_meta, cap, hipHostMallocDefault) != hipSuccess) return GPUHASH_ENOMEM;
     d.meta_cap = cap;
+    return GPUHASH_OK;
+}
+
+static int dev_reserve_ktab(Dev& d, size_t words) {
+    if (words <= d.ktab_cap) return GPUHASH_OK;
+    if (d.d_ktab) hipFree(d.d_ktab);
+    d.d_ktab = nullptr;
+    d.ktab_cap = 0;
+    if (hipMalloc(&d.d_ktab, words * sizeof(uint32_t)) != hipSuccess) return GPUHASH_ENOMEM;
+    d.ktab_cap = words;
     return GPUHASH_OK;
 }
 
@@ -162,15 +176,31 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
     std::memset(d.h_meta, 0, 8 * groups.size());
     uint32_t maxgrid = 1;
     std::vector<unsigned int> grids(groups.size());
+    // C2/J=0 tables: block B's words depend only on the digit count d, so one table per
+    // d serves every descriptor of that digit group; built by k_ktab from the device
+    // copy of the first such descriptor (at desc_at[g] + k * sizeof(LaunchDesc)).
+    struct Tab { int d; uint32_t off, R; size_t desc_byte; };
+    std::vector<Tab> tabs;
+    size_t tab_words = 0;
     for (size_t g = 0; g < groups.size(); g++) {
         auto* offs = reinterpret_cast<unsigned long long*>(d.h_meta + offs_at[g]);
         auto* descs = reinterpret_cast<LaunchDesc*>(d.h_meta + desc_at[g]);
         unsigned long long acc = 0;
         for (size_t k = 0; k < groups[g].idx.size(); k++) {
-            const LaunchDesc& D = plan[groups[g].idx[k]].desc;
+            const Launch& l = plan[groups[g].idx[k]];
+            const LaunchDesc& D = l.desc;
             offs[k] = acc;
             acc += (unsigned long long)((D.p_last - D.p_first) / (uint32_t)kBlock + 1u) * D.R;
             descs[k] = D;
+            if (l.C2 && l.J == 0) {
+                auto it = std::find_if(tabs.begin(), tabs.end(), [&](const Tab& t) { return t.d == l.d; });
+                if (it == tabs.end()) {
+                    tabs.push_back(Tab{l.d, (uint32_t)tab_words, D.R, desc_at[g] + k * sizeof(LaunchDesc)});
+                    tab_words += 64ull * D.R;
+                    it = tabs.end() - 1;
+                }
+                descs[k].tab_off = it->off;
+            }
         }
         offs[groups[g].idx.size()] = acc;
         unsigned int full = grid_for(groups[g].J, groups[g].C2, groups[g].EX, mode, d.ord);
@@ -182,7 +212,11 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
     }
     rc = dev_reserve(d, maxgrid, 2 * groups.size());
     if (rc) return rc;
+    if (tab_words && (rc = dev_reserve_ktab(d, tab_words))) return rc;
     HIPCHK(hipMemcpyAsync(d.d_meta, d.h_meta, bytes, hipMemcpyHostToDevice, d.stream));
+    for (const Tab& t : tabs)
+        HIPCHK(launch_ktab(reinterpret_cast<const LaunchDesc*>(d.d_meta + t.desc_byte), d.d_ktab + t.off,
+                           t.R, d.stream));
     HIPCHK(hipMemsetAsync(d.d_thresh, 0xFF, sizeof(unsigned long long), d.stream));
     HIPCHK(hipMemsetAsync(d.d_best, 0xFF, sizeof(Cand), d.stream));
     HIPCHK(hipMemsetAsync(d.d_ncand, 0, sizeof(unsigned int), d.stream));
@@ -202,6 +236,7 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
         a.ncand = d.d_ncand;
         a.dump = d_dump;
         a.dump_lo = lo;
+        a.ktab = d.d_ktab;
         a.grid = grids[g];
         HIPCHK(hipEventRecord(d.ev[2 * g], d.stream));
         HIPCHK(launch_scan(groups[g].J, groups[g].C2, groups[g].EX, mode, a));

@@ -24,6 +24,7 @@ struct ScanArgs {
     unsigned int* ncand;             // append counter
     unsigned long long* dump;        // MODE 1 only: per-nonce hashes
     unsigned long long dump_lo;      // MODE 1 only: nonce of dump[0]
+    const uint32_t* ktab;            // C2/J=0 only: per-r K+W tables (see LaunchDesc::tab_off)
     unsigned int grid;               // workgroups (<= resident capacity, see grid_for)
 };
 
@@ -32,6 +33,9 @@ unsigned int grid_for(int J, int C2, int EX, int mode, int device);
 
 // One persistent launch of the (J, C2, EX) variant over a.descs[0..ndesc).
 hipError_t launch_scan(int J, int C2, int EX, int mode, const ScanArgs& a);
+// Fills the uniform K+W table of a C2/J=0 descriptor: tab[64*r + t] = K[t] + W_t(r),
+// r in [0, D.R), for block B's words U with the loop digits of r inserted into W_0.
+hipError_t launch_ktab(const LaunchDesc* d_desc, uint32_t* tab, uint32_t R, hipStream_t stream);
 hipError_t launch_reduce(Cand* cands, unsigned int* ncand, Cand* best, hipStream_t stream);
 
 }  // namespace gpuhash

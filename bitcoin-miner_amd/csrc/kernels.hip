@@ -41,6 +41,24 @@ __global__ __launch_bounds__(1024) void k_reduce(Cand* __restrict__ cands,
     }
 }
 
+// Uniform schedule table of a C2/J=0 descriptor (one thread per loop value r):
+// tab[64*r + t] = K[t] + W_t, W = block B's uniform words with r's ASCII digits in W_0.
+__global__ __launch_bounds__(256) void k_ktab(const LaunchDesc* __restrict__ desc,
+                                              uint32_t* __restrict__ tab, uint32_t R) {
+    using namespace dev;
+    const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+    if (r >= R) return;
+    const LaunchDesc& D = *desc;
+    uint32_t w[64];
+#pragma unroll
+    for (int i = 0; i < 16; i++) w[i] = D.U[i];
+    w[0] |= (ascii4(r) & D.qmask) << D.loop_shift;
+    expand_full(w);
+    uint32_t* out = tab + 64ull * r;
+#pragma unroll
+    for (int t = 0; t < 64; t++) out[t] = K[t] + w[t];
+}
+
 template <int J, bool C2, bool EX, int MODE>
 static auto kfn() {
     return &k_scan<J, C2, EX, MODE>;
@@ -50,7 +68,7 @@ template <int J, bool C2, bool EX, int MODE>
 static hipError_t go(const ScanArgs& a) {
     hipLaunchKernelGGL((k_scan<J, C2, EX, MODE>), dim3(a.grid), dim3(256), 0, a.stream, a.descs,
                        a.offs, a.ndesc, a.work, a.gmin, a.gmax, a.thresh, a.cands, a.ncand, a.dump,
-                       a.dump_lo);
+                       a.dump_lo, a.ktab);
     return hipGetLastError();
 }
 
@@ -133,6 +151,12 @@ unsigned int grid_for(int J, int C2, int EX, int mode, int device) {
 hipError_t launch_scan(int J, int C2, int EX, int mode, const ScanArgs& a) {
     if (!valid_variant(J, C2, EX) || a.grid == 0 || a.ndesc <= 0) return hipErrorInvalidValue;
     return mode == 0 ? with_variant<0>(J, C2, EX, Launcher{a}) : with_variant<1>(J, C2, EX, Launcher{a});
+}
+
+hipError_t launch_ktab(const LaunchDesc* d_desc, uint32_t* tab, uint32_t R, hipStream_t stream) {
+    if (!d_desc || !tab || R == 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_ktab, dim3((R + 255u) / 256u), dim3(256), 0, stream, d_desc, tab, R);
+    return hipGetLastError();
 }
 
 hipError_t launch_reduce(Cand* cands, unsigned int* ncand, Cand* best, hipStream_t stream) {

@@ -53,7 +53,10 @@ struct LaunchDesc {
     uint32_t nrchunks; // ceil(R / rchunk)
     uint32_t p_first, p_last;  // lane values covered by this launch
     uint32_t r_first, r_last;  // r bounds at p_first / p_last (edges of [lo, hi])
-    uint32_t pad_;
+    // C2 with J == 0: every word of block B is wave-uniform (the lanes only vary block
+    // B-1), so its whole schedule K[t] + W_t(r) is a per-r table, built once per digit
+    // group by k_ktab; the scan reads row r at ktab + tab_off + 64*r (scalar loads).
+    uint32_t tab_off;
     uint64_t base;     // nonce = base + p·R + r
 };
 

@@ -128,9 +128,13 @@ struct WaveBest {
 template <int J, bool C2, bool EX, int MODE>
 __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint32_t r0, uint32_t r1,
                                          WaveBest& wb, unsigned long long* __restrict__ dump,
-                                         unsigned long long dump_lo) {
+                                         unsigned long long dump_lo, const uint32_t* __restrict__ ktab) {
     using namespace dev;
     constexpr DepTable<J> kDep{};
+    // C2 with the loop word at J = 0: block B carries no lane digit, so its message
+    // schedule is wave-uniform and comes precomputed from the per-r table (no per-nonce
+    // schedule work at all; the table row is read with scalar loads).
+    constexpr bool UT = C2 && J == 0;
     const uint32_t p = D.p_first + row * 256u + threadIdx.x;
 
     // ---- once per row: lane words and everything that does not read W_J ----
@@ -184,53 +188,71 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
     const uint32_t rhi = (p == D.p_last) ? D.r_last : D.R - 1u;
 
     for (uint32_t r = r0; r < r1; r++) {
-        const uint32_t WJ = D.U[J] | ((ascii4(r) & D.qmask) << D.loop_shift);
-        uint32_t w[64];
-#pragma unroll
-        for (int i = 0; i < 16; i++) w[i] = W[i];
-        w[J] = WJ;
-        // schedule: loop-invariant terms summed first so LICM hoists them
-        sfor<16, 64>([&](auto tc) {
-            constexpr int t = decltype(tc)::value;
-            constexpr bool d2 = kDep.v[t - 2], d7 = kDep.v[t - 7], d15 = kDep.v[t - 15], d16 = kDep.v[t - 16];
-            uint32_t x2, x15;
-            if constexpr (t - 2 == J) x2 = us1(w[t - 2]); else x2 = bs1(w[t - 2]);
-            if constexpr (t - 15 == J) x15 = us0(w[t - 15]); else x15 = bs0(w[t - 15]);
-            uint32_t inv = (d2 ? 0u : x2) + (d7 ? 0u : w[t - 7]) + (d15 ? 0u : x15) + (d16 ? 0u : w[t - 16]);
-            uint32_t var = (d2 ? x2 : 0u) + (d7 ? w[t - 7] : 0u) + (d15 ? x15 : 0u) + (d16 ? w[t - 16] : 0u);
-            w[t] = inv + var;
-        });
-        State x = s;
-        {   // round J: everything but W_J is loop-invariant
-            uint32_t inv = x.h + bS1(x.e) + ch(x.e, x.f, x.g) + K[J];
-            uint32_t t2 = bS0(x.a) + maj(x.a, x.b, x.c);
-            x.h = x.g; x.g = x.f; x.f = x.e; x.e = (x.d + inv) + WJ;
-            x.d = x.c; x.c = x.b; x.b = x.a; x.a = (inv + t2) + WJ;
-        }
-        sfor<J + 1, 63>([&](auto tc) {
-            constexpr int t = decltype(tc)::value;
-            if constexpr (t < 16) round_kw(x, K[t] + w[t]);   // uniform word: K+W folds
-            else round_kw(x, w[t] + K[t]);
-        });
         uint32_t H0, H1;
-        if constexpr (!EX) {
-            // round 63: e is dead; fold CV0 into the constant so a64 + CV0 is free
-            uint32_t t1 = x.h + w[63] + (K[63] + cv[0]) + ch(x.e, x.f, x.g) + bS1(x.e);
+        if constexpr (UT) {
+            const uint32_t* __restrict__ kw = ktab + D.tab_off + 64u * r;
+            State x = s;
+            {   // round 0: kw[0] = K[0] + W_0 is the only term that changes with r
+                uint32_t inv = x.h + bS1(x.e) + ch(x.e, x.f, x.g);
+                uint32_t t2 = bS0(x.a) + maj(x.a, x.b, x.c);
+                x.h = x.g; x.g = x.f; x.f = x.e; x.e = (x.d + inv) + kw[0];
+                x.d = x.c; x.c = x.b; x.b = x.a; x.a = (inv + t2) + kw[0];
+            }
+            sfor<1, 63>([&](auto tc) {
+                constexpr int t = decltype(tc)::value;
+                round_kw(x, kw[t]);
+            });
+            uint32_t t1 = x.h + kw[63] + cv[0] + ch(x.e, x.f, x.g) + bS1(x.e);
             H0 = t1 + bS0(x.a) + maj(x.a, x.b, x.c);
             H1 = cv[1] + x.a;
         } else {
-            round_kw(x, w[63] + K[63]);
-            State y{cv[0] + x.a, cv[1] + x.b, cv[2] + x.c, cv[3] + x.d,
-                    cv[4] + x.e, cv[5] + x.f, cv[6] + x.g, cv[7] + x.h};
-            const uint32_t y0 = y.a, y1 = y.b;
-            sfor<0, 63>([&](auto tc) {
+            const uint32_t WJ = D.U[J] | ((ascii4(r) & D.qmask) << D.loop_shift);
+            uint32_t w[64];
+#pragma unroll
+            for (int i = 0; i < 16; i++) w[i] = W[i];
+            w[J] = WJ;
+            // schedule: loop-invariant terms summed first so LICM hoists them
+            sfor<16, 64>([&](auto tc) {
                 constexpr int t = decltype(tc)::value;
-                round_kw(y, D.KWX[t]);
+                constexpr bool d2 = kDep.v[t - 2], d7 = kDep.v[t - 7], d15 = kDep.v[t - 15], d16 = kDep.v[t - 16];
+                uint32_t x2, x15;
+                if constexpr (t - 2 == J) x2 = us1(w[t - 2]); else x2 = bs1(w[t - 2]);
+                if constexpr (t - 15 == J) x15 = us0(w[t - 15]); else x15 = bs0(w[t - 15]);
+                uint32_t inv = (d2 ? 0u : x2) + (d7 ? 0u : w[t - 7]) + (d15 ? 0u : x15) + (d16 ? 0u : w[t - 16]);
+                uint32_t var = (d2 ? x2 : 0u) + (d7 ? w[t - 7] : 0u) + (d15 ? x15 : 0u) + (d16 ? w[t - 16] : 0u);
+                w[t] = inv + var;
             });
-            uint32_t t1 = y.h + D.KWX[63] + ch(y.e, y.f, y.g) + bS1(y.e);
-            H0 = y0 + t1 + bS0(y.a) + maj(y.a, y.b, y.c);
-            H1 = y1 + y.a;
-        }
+            State x = s;
+            {   // round J: everything but W_J is loop-invariant
+                uint32_t inv = x.h + bS1(x.e) + ch(x.e, x.f, x.g) + K[J];
+                uint32_t t2 = bS0(x.a) + maj(x.a, x.b, x.c);
+                x.h = x.g; x.g = x.f; x.f = x.e; x.e = (x.d + inv) + WJ;
+                x.d = x.c; x.c = x.b; x.b = x.a; x.a = (inv + t2) + WJ;
+            }
+            sfor<J + 1, 63>([&](auto tc) {
+                constexpr int t = decltype(tc)::value;
+                if constexpr (t < 16) round_kw(x, K[t] + w[t]);   // uniform word: K+W folds
+                else round_kw(x, w[t] + K[t]);
+            });
+            if constexpr (!EX) {
+                // round 63: e is dead; fold CV0 into the constant so a64 + CV0 is free
+                uint32_t t1 = x.h + w[63] + (K[63] + cv[0]) + ch(x.e, x.f, x.g) + bS1(x.e);
+                H0 = t1 + bS0(x.a) + maj(x.a, x.b, x.c);
+                H1 = cv[1] + x.a;
+            } else {
+                round_kw(x, w[63] + K[63]);
+                State y{cv[0] + x.a, cv[1] + x.b, cv[2] + x.c, cv[3] + x.d,
+                        cv[4] + x.e, cv[5] + x.f, cv[6] + x.g, cv[7] + x.h};
+                const uint32_t y0 = y.a, y1 = y.b;
+                sfor<0, 63>([&](auto tc) {
+                    constexpr int t = decltype(tc)::value;
+                    round_kw(y, D.KWX[t]);
+                });
+                uint32_t t1 = y.h + D.KWX[63] + ch(y.e, y.f, y.g) + bS1(y.e);
+                H0 = y0 + t1 + bS0(y.a) + maj(y.a, y.b, y.c);
+                H1 = y1 + y.a;
+            }
+        }  // !UT
 
 #ifdef GPUHASH_TIE_TEST_BITS
         // Test-only build (libgpuhash_tietest.so): keep only the top bits of the hash so
@@ -291,7 +313,8 @@ __global__ __launch_bounds__(256) void k_scan(const LaunchDesc* __restrict__ des
                                               Cand* __restrict__ cands,
                                               unsigned int* __restrict__ ncand,
                                               unsigned long long* __restrict__ dump,
-                                              unsigned long long dump_lo) {
+                                              unsigned long long dump_lo,
+                                              const uint32_t* __restrict__ ktab) {
     static_assert(J >= 0 && J < 16, "loop word index");
     static_assert(!C2 || J <= 1, "C2 layouts have the loop word at J <= 1");
     static_assert(!EX || J >= 13, "extra padding block only when the last digit is at byte >= 55");
@@ -329,7 +352,7 @@ __global__ __launch_bounds__(256) void k_scan(const LaunchDesc* __restrict__ des
             const uint32_t row = rel / D.R, r0 = rel - row * D.R;
             const unsigned long long left = end - x;
             const uint32_t r1 = (unsigned long long)(D.R - r0) < left ? D.R : r0 + (uint32_t)left;
-            scan_row<J, C2, EX, MODE>(D, row, r0, r1, wb, dump, dump_lo);
+            scan_row<J, C2, EX, MODE>(D, row, r0, r1, wb, dump, dump_lo, ktab);
             x += r1 - r0;
         }
     }
