@@ -192,7 +192,7 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
             offs[k] = acc;
             acc += (unsigned long long)((D.p_last - D.p_first) / (uint32_t)kBlock + 1u) * D.R;
             descs[k] = D;
-            if (l.C2 && l.J == 0) {
+            if (l.C2 == 1 && l.J == 0) {
                 auto it = std::find_if(tabs.begin(), tabs.end(), [&](const Tab& t) { return t.d == l.d; });
                 if (it == tabs.end()) {
                     tabs.push_back(Tab{l.d, (uint32_t)tab_words, D.R, desc_at[g] + k * sizeof(LaunchDesc)});

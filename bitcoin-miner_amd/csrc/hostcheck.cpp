@@ -87,14 +87,14 @@ int hostcheck_desc_hash(const uint8_t* msg, uint64_t len, uint64_t lower, uint64
     if (l.C2) {
         uint32_t V[64];
         std::memcpy(V, D.U1, 64);
-        if (J == 0) { V[15] |= alo & D.mask_lo; V[14] |= ahi & D.mask_hi; }
+        if (J == 0 || l.C2 == 2) { V[15] |= alo & D.mask_lo; V[14] |= ahi & D.mask_hi; }
         else { V[15] |= ahi & D.mask_hi; W[0] |= alo & D.mask_lo; }
         sha256_expand(V);
         std::memcpy(st, D.S1, 32);
         sha256_rounds(st, V, 14, 64);
         for (int i = 0; i < 8; i++) cv[i] = D.CV1[i] + st[i];
         std::memcpy(st, cv, 32);
-        if (J == 1) sha256_rounds(st, W, 0, 1);  // W[1..] unused by round 0
+        if (J == 1 && l.C2 == 1) sha256_rounds(st, W, 0, 1);  // W[1..] unused by round 0
     } else {
         std::memcpy(st, D.S0, 32);
         std::memcpy(cv, D.CV, 32);
@@ -107,9 +107,16 @@ int hostcheck_desc_hash(const uint8_t* msg, uint64_t len, uint64_t lower, uint64
             sha256_rounds(st, W, 0, 1);
         }
     }
-    W[J] = D.U[J] | ((ascii4(r) & D.qmask) << D.loop_shift);
+    int t0 = J;
+    if (l.C2 == 2) {  // two loop words: W_0 = 4 digits of r / R1, W_1 = digits of r % R1
+        W[0] = D.U[0] | ascii4(r / D.R1);
+        W[1] = D.U[1] | ((ascii4(r % D.R1) & D.qmask) << D.loop_shift);
+        t0 = 0;
+    } else {
+        W[J] = D.U[J] | ((ascii4(r) & D.qmask) << D.loop_shift);
+    }
     sha256_expand(W);
-    sha256_rounds(st, W, J, 64);
+    sha256_rounds(st, W, t0, 64);
     uint32_t y[8];
     for (int i = 0; i < 8; i++) y[i] = cv[i] + st[i];
     if (l.EX) {

@@ -59,12 +59,12 @@ __global__ __launch_bounds__(256) void k_ktab(const LaunchDesc* __restrict__ des
     for (int t = 0; t < 64; t++) out[t] = K[t] + w[t];
 }
 
-template <int J, bool C2, bool EX, int MODE>
+template <int J, int C2, bool EX, int MODE>
 static auto kfn() {
     return &k_scan<J, C2, EX, MODE>;
 }
 
-template <int J, bool C2, bool EX, int MODE>
+template <int J, int C2, bool EX, int MODE>
 static hipError_t go(const ScanArgs& a) {
     hipLaunchKernelGGL((k_scan<J, C2, EX, MODE>), dim3(a.grid), dim3(256), 0, a.stream, a.descs,
                        a.offs, a.ndesc, a.work, a.gmin, a.gmax, a.thresh, a.cands, a.ncand, a.dump,
@@ -72,7 +72,7 @@ static hipError_t go(const ScanArgs& a) {
     return hipGetLastError();
 }
 
-template <int J, bool C2, bool EX, int MODE>
+template <int J, int C2, bool EX, int MODE>
 static unsigned int occ(int device) {
     // cached per (variant, device): resident blocks per CU x CUs.  Device threads may
     // race to fill an entry; they compute the same value.
@@ -93,52 +93,54 @@ static unsigned int occ(int device) {
 // Expands a runtime (J, C2, EX) into the matching template instance and applies F.
 template <int MODE, class F>
 static auto with_variant(int J, int C2, int EX, F&& f) {
+    if (C2 == 2) return f.template operator()<1, 2, false, MODE>();
     if (C2) {
         switch (J) {
-            case 0: return f.template operator()<0, true, false, MODE>();
-            default: return f.template operator()<1, true, false, MODE>();
+            case 0: return f.template operator()<0, 1, false, MODE>();
+            default: return f.template operator()<1, 1, false, MODE>();
         }
     }
     if (EX) {
         switch (J) {
-            case 13: return f.template operator()<13, false, true, MODE>();
-            case 14: return f.template operator()<14, false, true, MODE>();
-            default: return f.template operator()<15, false, true, MODE>();
+            case 13: return f.template operator()<13, 0, true, MODE>();
+            case 14: return f.template operator()<14, 0, true, MODE>();
+            default: return f.template operator()<15, 0, true, MODE>();
         }
     }
     switch (J) {
-        case 0: return f.template operator()<0, false, false, MODE>();
-        case 1: return f.template operator()<1, false, false, MODE>();
-        case 2: return f.template operator()<2, false, false, MODE>();
-        case 3: return f.template operator()<3, false, false, MODE>();
-        case 4: return f.template operator()<4, false, false, MODE>();
-        case 5: return f.template operator()<5, false, false, MODE>();
-        case 6: return f.template operator()<6, false, false, MODE>();
-        case 7: return f.template operator()<7, false, false, MODE>();
-        case 8: return f.template operator()<8, false, false, MODE>();
-        case 9: return f.template operator()<9, false, false, MODE>();
-        case 10: return f.template operator()<10, false, false, MODE>();
-        case 11: return f.template operator()<11, false, false, MODE>();
-        case 12: return f.template operator()<12, false, false, MODE>();
-        default: return f.template operator()<13, false, false, MODE>();
+        case 0: return f.template operator()<0, 0, false, MODE>();
+        case 1: return f.template operator()<1, 0, false, MODE>();
+        case 2: return f.template operator()<2, 0, false, MODE>();
+        case 3: return f.template operator()<3, 0, false, MODE>();
+        case 4: return f.template operator()<4, 0, false, MODE>();
+        case 5: return f.template operator()<5, 0, false, MODE>();
+        case 6: return f.template operator()<6, 0, false, MODE>();
+        case 7: return f.template operator()<7, 0, false, MODE>();
+        case 8: return f.template operator()<8, 0, false, MODE>();
+        case 9: return f.template operator()<9, 0, false, MODE>();
+        case 10: return f.template operator()<10, 0, false, MODE>();
+        case 11: return f.template operator()<11, 0, false, MODE>();
+        case 12: return f.template operator()<12, 0, false, MODE>();
+        default: return f.template operator()<13, 0, false, MODE>();
     }
 }
 
 static bool valid_variant(int J, int C2, int EX) {
-    if (C2) return !EX && (J == 0 || J == 1);
+    if (C2 == 2) return !EX && J == 1;
+    if (C2) return C2 == 1 && !EX && (J == 0 || J == 1);
     if (EX) return J >= 13 && J <= 15;
     return J >= 0 && J <= 13;  // J = 14, 15 always need the extra block
 }
 
 struct Launcher {
     const ScanArgs& a;
-    template <int J, bool C2, bool EX, int MODE>
+    template <int J, int C2, bool EX, int MODE>
     hipError_t operator()() const { return go<J, C2, EX, MODE>(a); }
 };
 
 struct Occupancy {
     int device;
-    template <int J, bool C2, bool EX, int MODE>
+    template <int J, int C2, bool EX, int MODE>
     unsigned int operator()() const { return occ<J, C2, EX, MODE>(device); }
 };
 

@@ -111,6 +111,7 @@ namespace {
 
 struct GroupLayout {
     int d, J, q, s, C2, EX;
+    int q1;      // C2 = 2: digits of W_1 (q = 4 + q1)
     uint64_t B;  // index of the block holding the last digit
 };
 
@@ -132,6 +133,19 @@ GroupLayout layout_for(uint64_t m, int d) {
     // digit bytes of block B that precede word J
     uint64_t nbB = (f_abs >= wstart) ? 0 : wstart - std::max(f_abs, blkB);
     g.C2 = (uint64_t)g.s > nbB;
+    // J = 1 with lanes spilling into block B-1: W_0 is four digits.  When block B-1 holds
+    // at least 3 digits (>= 1000 lane values, rows stay full), move W_0's digits into the
+    // loop so block B carries loop digits only (C2 = 2: uniform schedule, no per-nonce
+    // schedule work); the lanes take the digits at the end of block B-1.
+    if (g.C2 && g.J == 1) {
+        const int nb1 = d - 4 - g.q;  // digits in block B-1 and earlier
+        if (nb1 >= 3) {
+            g.C2 = 2;
+            g.q1 = g.q;
+            g.q = 4 + g.q;
+            g.s = std::min(std::min(kMaxLane, nb1), kMaxLaunchDigitsU2 - g.q);
+        }
+    }
     return g;
 }
 
@@ -197,7 +211,8 @@ void build_launch(const uint8_t* msg, uint64_t m, const GroupLayout& g, uint64_t
     }
     D.mask_lo = low_bytes_mask(std::min(s, 4));
     D.mask_hi = low_bytes_mask(s - 4);
-    D.qmask = low_bytes_mask(q);
+    D.qmask = low_bytes_mask(g.C2 == 2 ? g.q1 : q);
+    D.R1 = g.C2 == 2 ? (uint32_t)pow10u(g.q1) : 1u;
     const int e = (int)((L - 1) % 64);
     D.loop_shift = (uint32_t)(3 - e % 4) * 8u;
     const uint64_t R = pow10u(q), P = pow10u(s);
@@ -251,8 +266,11 @@ double group_cost(uint64_t msg_len, int d) {
     GroupLayout g = layout_for(msg_len, d);
     // relative VALU work per nonce: one final-block compression, +0.7 for the extra
     // constant block, + the per-lane block B-1 compression amortised over R nonces.
+    // (measured per-layout rates, profiles/r01_layout_sweep.jsonl: plain 32-39 GH/s,
+    // uniform-schedule C2 ~45, extra padding block ~20.5)
     double c = 1.0;
     if (g.EX) c += 0.7;
+    if (g.C2 == 2 || (g.C2 == 1 && g.J == 0)) c = 0.75;
     if (g.C2) c += 0.9 / (double)pow10u(g.q);
     else c += 0.2 / (double)std::min<uint64_t>(pow10u(g.q), 100);
     return c;

@@ -13,6 +13,9 @@
 //                    W_J of the final block B -> the only per-nonce message word
 //     lane digits p: the s (0..8) digits just before word J, i.e. virtual words J-1 and
 //                    J-2 (these may fall into block B-1: "C2" layouts)
+//     (C2 = 2, J = 1: the loop takes the 4 digits of W_0 as well -- q = 4 + digits of
+//      W_1, up to 8 -- so block B holds loop digits only and its schedule is uniform;
+//      the lanes then take only digits of block B-1)
 //     uniform     : prefix bytes, H's digits, 0x80, zero pad, bit length -> host
 //                    precomputes the midstate, the uniform words and the rounds that
 //                    only read uniform words
@@ -57,12 +60,14 @@ struct LaunchDesc {
     // B-1), so its whole schedule K[t] + W_t(r) is a per-r table, built once per digit
     // group by k_ktab; the scan reads row r at ktab + tab_off + 64*r (scalar loads).
     uint32_t tab_off;
+    uint32_t R1;       // C2 = 2: 10^(digits of W_1); r = (W_0 digits) * R1 + (W_1 digits)
+    uint32_t pad_;
     uint64_t base;     // nonce = base + p·R + r
 };
 
 struct Launch {
     int J;          // loop word index in block B
-    int C2;         // lane block B-1 compressed per lane
+    int C2;         // 1: lane block B-1 compressed per lane; 2: and W_0, W_1 are loop words
     int EX;         // extra constant padding block
     int d, q, s;    // digits, loop digits, lane digits
     int c;          // 64-byte blocks that hold nonce digits (the SURVEY 8(d) "c")
@@ -75,6 +80,8 @@ struct Launch {
 static constexpr int kMaxLane = 8;
 static constexpr int kBlock = 256;
 static constexpr int kMaxLaunchDigits = 10;   // s + q <= 10  -> <= 10^10 nonces per launch
+// C2 = 2 launches: s + q <= 12 still keeps rows * R = ceil(10^s / 256) * 10^q < 2^32
+static constexpr int kMaxLaunchDigitsU2 = 12;
 
 // Plans [lower, upper] (inclusive, lower <= upper) of `msg`.  `rchunk_max` caps the r
 // values per work item (0 = default).  Appends to `out`.

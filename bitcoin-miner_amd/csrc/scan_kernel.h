@@ -124,17 +124,44 @@ struct WaveBest {
     uint32_t T;
 };
 
+// Rounds 0..63 of block B when its whole message schedule is wave-uniform (C2 layouts
+// whose loop digits are the only digits in block B): kw[t] = K[t] + W_t comes from a
+// table, the per-lane input is the state s after block B-1 (= cv), so a nonce costs 64
+// rounds and no schedule work.  Round 0 reuses the per-row part `inv0` (everything but
+// kw[0]); round 63 skips e and folds CV0.
+template <class KW>
+__device__ __forceinline__ void ut_hash(const dev::State& s, const uint32_t (&cv)[8], uint32_t inv0,
+                                        uint32_t t20, KW&& kw, uint32_t& H0, uint32_t& H1) {
+    using namespace dev;
+    dev::State x = s;
+    const uint32_t k0 = kw(0);
+    x.h = x.g; x.g = x.f; x.f = x.e; x.e = (x.d + inv0) + k0;
+    x.d = x.c; x.c = x.b; x.b = x.a; x.a = (inv0 + t20) + k0;
+    sfor<1, 63>([&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        round_kw(x, kw(t));
+    });
+    const uint32_t t1 = x.h + kw(63) + cv[0] + ch(x.e, x.f, x.g) + bS1(x.e);
+    H0 = t1 + bS0(x.a) + maj(x.a, x.b, x.c);
+    H1 = cv[1] + x.a;
+}
+
 // One row of one launch: 256 consecutive lane values p (row) x loop values [r0, r1).
-template <int J, bool C2, bool EX, int MODE>
+//
+// C2 = 0: lane digits in words J-2, J-1 of block B, loop digits in W_J.
+// C2 = 1: lane digits spill into block B-1 (compressed per lane, once per row); for J = 0
+//         block B holds only loop digits, so its schedule is the per-r table `ktab`
+//         (built by k_ktab, read with scalar loads).
+// C2 = 2: (J = 1) block B's W_0 and W_1 hold only LOOP digits (r = W_0 digits * R1 + W_1
+//         digits) and the lanes vary block B-1 only; the uniform schedules of 64 loop
+//         values at a time are built by wave 0 into LDS and shared by the 4 waves.
+template <int J, int C2, bool EX, int MODE>
 __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint32_t r0, uint32_t r1,
                                          WaveBest& wb, unsigned long long* __restrict__ dump,
                                          unsigned long long dump_lo, const uint32_t* __restrict__ ktab) {
     using namespace dev;
     constexpr DepTable<J> kDep{};
-    // C2 with the loop word at J = 0: block B carries no lane digit, so its message
-    // schedule is wave-uniform and comes precomputed from the per-r table (no per-nonce
-    // schedule work at all; the table row is read with scalar loads).
-    constexpr bool UT = C2 && J == 0;
+    constexpr bool UT = C2 == 2 || (C2 == 1 && J == 0);  // uniform block-B schedule
     const uint32_t p = D.p_first + row * 256u + threadIdx.x;
 
     // ---- once per row: lane words and everything that does not read W_J ----
@@ -145,11 +172,11 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
     for (int i = 0; i < 16; i++) W[i] = D.U[i];
     State s;
     uint32_t cv[8];
-    if constexpr (C2) {
+    if constexpr (C2 != 0) {
         uint32_t V[64];
 #pragma unroll
         for (int i = 0; i < 16; i++) V[i] = D.U1[i];
-        if constexpr (J == 0) {
+        if constexpr (UT) {  // every lane digit sits at the end of block B-1
             V[15] |= alo & D.mask_lo;
             V[14] |= ahi & D.mask_hi;
         } else {
@@ -165,7 +192,7 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
         cv[0] = D.CV1[0] + s.a; cv[1] = D.CV1[1] + s.b; cv[2] = D.CV1[2] + s.c; cv[3] = D.CV1[3] + s.d;
         cv[4] = D.CV1[4] + s.e; cv[5] = D.CV1[5] + s.f; cv[6] = D.CV1[6] + s.g; cv[7] = D.CV1[7] + s.h;
         s = State{cv[0], cv[1], cv[2], cv[3], cv[4], cv[5], cv[6], cv[7]};
-        if constexpr (J == 1) round_kw(s, K[0] + W[0]);
+        if constexpr (!UT && J == 1) round_kw(s, K[0] + W[0]);
     } else {
         s = State{D.S0[0], D.S0[1], D.S0[2], D.S0[3], D.S0[4], D.S0[5], D.S0[6], D.S0[7]};
 #pragma unroll
@@ -180,6 +207,12 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
             round_kw(s, K[0] + W[0]);
         }
     }
+    // UT layouts: round 0 of block B without its K+W term (per row)
+    uint32_t inv0 = 0, t20 = 0;
+    if constexpr (UT) {
+        inv0 = s.h + bS1(s.e) + ch(s.e, s.f, s.g);
+        t20 = bS0(s.a) + maj(s.a, s.b, s.c);
+    }
 
     // Edge handling: only the first / last lane of a launch has a partial r range, and
     // lanes past p_last are idle.  Checked only in the (rare) slow path.
@@ -187,24 +220,83 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
     const uint32_t rlo = (p == D.p_first) ? D.r_first : 0u;
     const uint32_t rhi = (p == D.p_last) ? D.r_last : D.R - 1u;
 
+    // Per-nonce bookkeeping: dump (MODE 1) or the exact lexicographic running best with
+    // the wave-uniform pruning test (MODE 0).
+    auto finish = [&](uint32_t r, uint32_t H0, uint32_t H1) {
+#ifdef GPUHASH_TIE_TEST_BITS
+        // Test-only build (libgpuhash_tietest.so): keep only the top bits of the hash so
+        // equal keys are common and every reduction level's lowest-nonce rule is exercised.
+        H0 >>= (32 - GPUHASH_TIE_TEST_BITS);
+        H1 = 0;
+#endif
+        if constexpr (MODE == 1) {
+            if (lane_ok && r >= rlo && r <= rhi) {
+                unsigned long long n = D.base + (unsigned long long)p * D.R + r;
+                dump[n - dump_lo] = ((unsigned long long)H0 << 32) | H1;
+            }
+        } else {
+            unsigned long long m = __builtin_amdgcn_ballot_w64(H0 <= wb.T);
+            if (m) {  // wave-uniform, rare once T has settled
+                const bool ok = lane_ok && r >= rlo && r <= rhi;
+                m = __builtin_amdgcn_ballot_w64(H0 <= wb.T && ok);
+                while (m) {
+                    const int l = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const uint32_t h0 = __builtin_amdgcn_readlane(H0, l);
+                    const uint32_t h1 = __builtin_amdgcn_readlane(H1, l);
+                    const uint32_t pl = __builtin_amdgcn_readlane(p, l);
+                    const unsigned long long hh = ((unsigned long long)h0 << 32) | h1;
+                    const unsigned long long nn = D.base + (unsigned long long)pl * D.R + r;
+                    if (hh < wb.h || (hh == wb.h && nn < wb.n)) {
+                        wb.h = hh;
+                        wb.n = nn;
+                        wb.T = h0 < wb.T ? h0 : wb.T;
+                    }
+                }
+            }
+        }
+    };
+
+    if constexpr (C2 == 2) {
+        // 64 loop values per batch: wave 0 lane j builds the K+W schedule of r = rb + j
+        // (row stride 68 words keeps 16-byte alignment for the broadcast reads).
+        __shared__ uint4 sh_kw[64][17];
+        for (uint32_t rb = r0; rb < r1; rb += 64u) {
+            const uint32_t nb = r1 - rb < 64u ? r1 - rb : 64u;
+            __syncthreads();  // the previous batch has been consumed by every wave
+            if (threadIdx.x < nb) {
+                const uint32_t r = rb + threadIdx.x;
+                const uint32_t m = r / D.R1, q = r - m * D.R1;
+                uint32_t w[64];
+#pragma unroll
+                for (int i = 0; i < 16; i++) w[i] = D.U[i];
+                w[0] |= ascii4(m);
+                w[1] |= (ascii4(q) & D.qmask) << D.loop_shift;
+                expand_full(w);
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    sh_kw[threadIdx.x][i] = make_uint4(K[4 * i] + w[4 * i], K[4 * i + 1] + w[4 * i + 1],
+                                                       K[4 * i + 2] + w[4 * i + 2], K[4 * i + 3] + w[4 * i + 3]);
+            }
+            __syncthreads();
+            for (uint32_t j = 0; j < nb; j++) {
+                const uint4* kr = sh_kw[j];
+                uint32_t H0, H1;
+                ut_hash(s, cv, inv0, t20, [&](int t) {
+                    const uint4 v = kr[t >> 2];
+                    return (t & 3) == 0 ? v.x : (t & 3) == 1 ? v.y : (t & 3) == 2 ? v.z : v.w;
+                }, H0, H1);
+                finish(rb + j, H0, H1);
+            }
+        }
+        return;
+    }
+
     for (uint32_t r = r0; r < r1; r++) {
         uint32_t H0, H1;
         if constexpr (UT) {
             const uint32_t* __restrict__ kw = ktab + D.tab_off + 64u * r;
-            State x = s;
-            {   // round 0: kw[0] = K[0] + W_0 is the only term that changes with r
-                uint32_t inv = x.h + bS1(x.e) + ch(x.e, x.f, x.g);
-                uint32_t t2 = bS0(x.a) + maj(x.a, x.b, x.c);
-                x.h = x.g; x.g = x.f; x.f = x.e; x.e = (x.d + inv) + kw[0];
-                x.d = x.c; x.c = x.b; x.b = x.a; x.a = (inv + t2) + kw[0];
-            }
-            sfor<1, 63>([&](auto tc) {
-                constexpr int t = decltype(tc)::value;
-                round_kw(x, kw[t]);
-            });
-            uint32_t t1 = x.h + kw[63] + cv[0] + ch(x.e, x.f, x.g) + bS1(x.e);
-            H0 = t1 + bS0(x.a) + maj(x.a, x.b, x.c);
-            H1 = cv[1] + x.a;
+            ut_hash(s, cv, inv0, t20, [&](int t) { return kw[t]; }, H0, H1);
         } else {
             const uint32_t WJ = D.U[J] | ((ascii4(r) & D.qmask) << D.loop_shift);
             uint32_t w[64];
@@ -252,40 +344,8 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
                 H0 = y0 + t1 + bS0(y.a) + maj(y.a, y.b, y.c);
                 H1 = y1 + y.a;
             }
-        }  // !UT
-
-#ifdef GPUHASH_TIE_TEST_BITS
-        // Test-only build (libgpuhash_tietest.so): keep only the top bits of the hash so
-        // equal keys are common and every reduction level's lowest-nonce rule is exercised.
-        H0 >>= (32 - GPUHASH_TIE_TEST_BITS);
-        H1 = 0;
-#endif
-        if constexpr (MODE == 1) {
-            if (lane_ok && r >= rlo && r <= rhi) {
-                unsigned long long n = D.base + (unsigned long long)p * D.R + r;
-                dump[n - dump_lo] = ((unsigned long long)H0 << 32) | H1;
-            }
-        } else {
-            unsigned long long m = __builtin_amdgcn_ballot_w64(H0 <= wb.T);
-            if (m) {  // wave-uniform, rare once T has settled
-                const bool ok = lane_ok && r >= rlo && r <= rhi;
-                m = __builtin_amdgcn_ballot_w64(H0 <= wb.T && ok);
-                while (m) {
-                    const int l = __builtin_ctzll(m);
-                    m &= m - 1;
-                    const uint32_t h0 = __builtin_amdgcn_readlane(H0, l);
-                    const uint32_t h1 = __builtin_amdgcn_readlane(H1, l);
-                    const uint32_t pl = __builtin_amdgcn_readlane(p, l);
-                    const unsigned long long hh = ((unsigned long long)h0 << 32) | h1;
-                    const unsigned long long nn = D.base + (unsigned long long)pl * D.R + r;
-                    if (hh < wb.h || (hh == wb.h && nn < wb.n)) {
-                        wb.h = hh;
-                        wb.n = nn;
-                        wb.T = h0 < wb.T ? h0 : wb.T;
-                    }
-                }
-            }
         }
+        finish(r, H0, H1);
     }
 }
 
@@ -304,7 +364,7 @@ __device__ __forceinline__ unsigned long long uniform64(unsigned long long v) {
 // amortise the per-row setup and the last ones are short, which keeps the tail of the
 // launch to ~gmin iterations.  The wave-uniform best (and its pruning word) persists
 // across pieces; each workgroup appends one 16-byte candidate at the end if it found one.
-template <int J, bool C2, bool EX, int MODE>
+template <int J, int C2, bool EX, int MODE>
 __global__ __launch_bounds__(256) void k_scan(const LaunchDesc* __restrict__ descs,
                                               const unsigned long long* __restrict__ offs,
                                               int ndesc, unsigned long long* __restrict__ work,
@@ -317,6 +377,7 @@ __global__ __launch_bounds__(256) void k_scan(const LaunchDesc* __restrict__ des
                                               const uint32_t* __restrict__ ktab) {
     static_assert(J >= 0 && J < 16, "loop word index");
     static_assert(!C2 || J <= 1, "C2 layouts have the loop word at J <= 1");
+    static_assert(C2 != 2 || J == 1, "two-word uniform loop only with the loop word at J = 1");
     static_assert(!EX || J >= 13, "extra padding block only when the last digit is at byte >= 55");
     __shared__ unsigned long long sh_grab[2];
     __shared__ unsigned long long sh_best[4][2];

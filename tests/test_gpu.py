@@ -62,6 +62,40 @@ def test_hash_range_bit_exact(engine, oracle):
         assert bad.size == 0, (len(m), lo, cnt, int(bad[0]) + lo)
 
 
+@pytest.mark.parametrize("mlen,d,c2,j", [
+    (58, 10, 2, 1), (59, 10, 2, 1), (60, 10, 2, 1), (56, 12, 2, 1), (59, 12, 2, 1),  # two-word loop
+    (120, 10, 1, 0), (54, 10, 1, 0), (119, 12, 1, 0),                                # K+W table
+])
+def test_uniform_schedule_layouts(engine, oracle, mlen, d, c2, j):
+    """Layouts whose final block holds loop digits only (its schedule is built once per
+    loop value: C2=1/J=0 from the k_ktab table, C2=2/J=1 in LDS): per-nonce parity over
+    windows where the W_1 and W_0 loop digits roll over, and min parity."""
+    rng = random.Random(mlen * 100 + d)
+    m = bytes(rng.randrange(32, 127) for _ in range(mlen))
+    base = 10 ** (d - 1) + rng.randrange(10 ** (d - 2))
+    engine.min(m, base, base + 1000)
+    assert any(r["C2"] == c2 and r["J"] == j for r in engine.launches()), engine.launches()
+    for lo in (base - base % 10 ** 4 - 700, base - base % 10 ** 8 - 3000, base + 12345):
+        got = engine.hash_range(m, lo, 6000)
+        want = oracle.hash_range(m, lo, 6000)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (mlen, d, lo, int(bad[0]) + lo if bad.size else None)
+    for lo, hi in ((base, base + 2_000_000), (base - base % 10 ** 6 - 77, base - base % 10 ** 6 + 300_000)):
+        assert engine.min(m, lo, hi) == oracle.min(m, lo, hi), (mlen, d, lo, hi)
+
+
+def test_ktab_several_digit_groups_in_one_call(engine, oracle):
+    # m = 55: d = 9, 10, 11 are all C2/J=0 layouts, so a window across 10^9 (or 10^10)
+    # builds two K+W tables (one per digit count) for the same launch group
+    m = M120[:55]
+    for x in (10 ** 9, 10 ** 10):
+        assert engine.min(m, x - 40_000, x + 40_000) == oracle.min(m, x - 40_000, x + 40_000)
+        recs = [r for r in engine.launches() if r["C2"] == 1 and r["J"] == 0]
+        assert recs and recs[0]["nonces"] == 80_001, engine.launches()
+        got = engine.hash_range(m, x - 3000, 6000)
+        assert (got == oracle.hash_range(m, x - 3000, 6000)).all()
+
+
 def test_min_matches_oracle_random(engine, oracle):
     rng = random.Random(9)
     for _ in range(120):

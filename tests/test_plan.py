@@ -66,7 +66,10 @@ def test_plan_tiles_range_and_layouts_are_legal(hc):
         for x, y in zip(p, p[1:]):
             assert y.lo == x.hi + 1
         for l in p:
-            assert 1 <= l.q <= 4 and 0 <= l.s <= 8 and l.s + l.q <= 10
+            if l.C2 == 2:  # two-word uniform loop: W_0 (4 digits) + W_1 (1..4 digits)
+                assert l.J == 1 and 5 <= l.q <= 8 and 3 <= l.s <= 8 and l.s + l.q <= 12
+            else:
+                assert 1 <= l.q <= 4 and 0 <= l.s <= 8 and l.s + l.q <= 10
             assert not (l.C2 and l.J > 1) and not (l.EX and l.J < 13) and not (l.C2 and l.EX)
             assert l.R == 10 ** l.q
             assert l.lo == l.base + l.p_first * l.R + l.r_first
@@ -89,8 +92,8 @@ def test_descriptor_replay_matches_oracle(hc, oracle):
             seen.add((l.J, l.C2, l.EX))
             for n in {l.lo, l.hi, rng.randrange(l.lo, l.hi + 1)}:
                 assert desc_hash(hc, m, a, b, i, n) == oracle.hash(m, n), (m, a, b, i, n)
-    # every one of the 19 reachable (J, C2, EX) variants was exercised
-    assert len(seen) == 19, sorted(seen)
+    # every one of the 20 reachable (J, C2, EX) variants was exercised
+    assert len(seen) == 20, sorted(seen)
 
 
 @pytest.mark.parametrize("mlen", [0, 8, 44, 45, 53, 54, 55, 56, 63, 64, 110, 119, 120, 127, 128, 180])
