@@ -102,7 +102,7 @@ def pmc_traffic(key) -> float | None:
     try:
         with open(path) as f:
             t = json.load(f)
-        return t["kernels"][f"k_scan<{key[0]}, {bool(key[1])}, {bool(key[2])}, 0>".lower()]["hbm_bytes_per_launch"]
+        return t["kernels"][f"k_scan<{key[0]}, {int(key[1])}, {str(bool(key[2])).lower()}, 0>"]["hbm_bytes_per_launch"]
     except (OSError, KeyError, ValueError):
         return None
 
