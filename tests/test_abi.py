@@ -90,3 +90,30 @@ def test_no_silent_cpu_fallback(lib):
     with pytest.raises(gpuhash.GpuHashError) as e:
         gpuhash.Engine()
     assert e.value.rc == gpuhash.GPUHASH_ENODEV
+
+
+CLI = os.path.join(ROOT, "bitcoin-miner_amd", "lib", "gpuhash_cli")
+
+
+def _gpu_visible():
+    try:
+        import torch
+        return torch.cuda.device_count() > 0
+    except Exception:
+        return False
+
+
+def test_plain_c_client_links_and_fails_loudly_without_gpu():
+    """The C client (the cgo binding's call sequence, no Python in the process) links
+    against the in-tree library; with no gfx950 device it exits with the ENODEV error
+    instead of computing anything on the host."""
+    if not os.path.exists(CLI):
+        subprocess.check_call(["make", "-C", os.path.join(ROOT, "bitcoin-miner_amd"), "lib/gpuhash_cli"])
+    v = subprocess.run([CLI, "--version"], capture_output=True, text=True)
+    assert v.returncode == 0 and v.stdout.startswith("gpuhash ")
+    assert subprocess.run([CLI, "bradfitz", "5"], capture_output=True).returncode == 2
+    assert subprocess.run([CLI, "bradfitz", "-1", "5"], capture_output=True).returncode == 2
+    if _gpu_visible():
+        pytest.skip("a GPU is visible: the no-device path is not reachable here")
+    r = subprocess.run([CLI, "bradfitz", "0", "9999"], capture_output=True, text=True)
+    assert r.returncode == 3 and "no usable gfx950" in r.stderr and r.stdout == ""

@@ -174,6 +174,26 @@ def test_multi_device_sharding_and_host_argmin(engine, oracle):
         assert multi.min(b"bradfitz", 0, 9999) == oracle.min(b"bradfitz", 0, 9999)
 
 
+def test_plain_c_client_through_the_abi(oracle):
+    """gpuhash_cli: a C process with no Python/torch, making the cgo binding's calls."""
+    import os
+    import subprocess
+    cli = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "bitcoin-miner_amd", "lib", "gpuhash_cli")
+    out = subprocess.run([cli, "bradfitz", "0", "9999"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip() == "Result 1419516646206828 9898"
+    m = M120[:58].decode()
+    out = subprocess.run([cli, m, "999000000", "1001000000"], capture_output=True, text=True, timeout=120)
+    h, n = oracle.min(m.encode(), 999000000, 1001000000)
+    assert out.returncode == 0 and out.stdout.strip() == f"Result {h} {n}", out.stderr
+    out = subprocess.run([cli, "--range", "msg", "0", "3"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.split() == ["13781283048668101583", "4754799531757243342",
+                                                          "5611725180048225792"]
+    out = subprocess.run([cli, "bradfitz", "10", "5"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 3 and "invalid argument" in out.stderr
+
+
 def test_native_library_is_the_one_loaded(engine):
     import gpuhash
     maps = open("/proc/self/maps").read()
