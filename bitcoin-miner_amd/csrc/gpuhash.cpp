@@ -50,6 +50,7 @@ struct Dev {
 
 struct gpuhash_ctx {
     std::vector<Dev> devs;
+    int policy = kLayoutAuto;
     gpuhash_stats last{};
     std::vector<gpuhash_launch_record> recs;
 };
@@ -134,14 +135,14 @@ static int dev_reserve(Dev& d, uint32_t cap, size_t nev) {
 // scan_kernel.h), followed by the candidate reduce.  One 16-byte copy back at the end.
 // mode 1 writes per-nonce hashes to d_dump instead.
 static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi,
-                   uint32_t rchunk, int mode, unsigned long long* d_dump) {
+                   uint32_t rchunk, int mode, unsigned long long* d_dump, int policy) {
     d.used = true;
     d.kernel_ms = 0;
     d.launches = 0;
     d.recs.clear();
     HIPCHK(hipSetDevice(d.ord));
     std::vector<Launch> plan;
-    plan_range(msg, len, lo, hi, plan, rchunk);
+    plan_range(msg, len, lo, hi, plan, rchunk, policy);
 
     struct Group {
         int J, C2, EX;
@@ -305,6 +306,12 @@ int gpuhash_open(const int* devices, int ndevices, gpuhash_ctx** out) {
 
 int gpuhash_ndevices(const gpuhash_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
 
+int gpuhash_set_layout_policy(gpuhash_ctx* ctx, int policy) {
+    if (!ctx || policy < GPUHASH_LAYOUT_AUTO || policy > GPUHASH_LAYOUT_CLASSIC) return GPUHASH_EINVAL;
+    ctx->policy = policy;
+    return GPUHASH_OK;
+}
+
 int gpuhash_min_ex(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uint64_t lower,
                    uint64_t upper, uint32_t rchunk, uint64_t* out_hash, uint64_t* out_nonce) {
     if (!ctx || !out_hash || !out_nonce || (msg_len && !msg)) return GPUHASH_EINVAL;
@@ -315,14 +322,15 @@ int gpuhash_min_ex(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uint64_
     std::vector<Shard> sh = shard_range(msg_len, lower, upper, n);
     for (auto& d : ctx->devs) { d.used = false; d.rc = GPUHASH_OK; d.kernel_ms = 0; d.launches = 0; }
     if (n == 1) {
-        ctx->devs[0].rc = dev_run(ctx->devs[0], msg, msg_len, lower, upper, rchunk, 0, nullptr);
+        ctx->devs[0].rc = dev_run(ctx->devs[0], msg, msg_len, lower, upper, rchunk, 0, nullptr, ctx->policy);
     } else {
         std::vector<std::thread> th;
         for (int i = 0; i < n; i++) {
             if (sh[(size_t)i].empty) continue;
             th.emplace_back([&, i] {
                 Dev& d = ctx->devs[(size_t)i];
-                d.rc = dev_run(d, msg, msg_len, sh[(size_t)i].lo, sh[(size_t)i].hi, rchunk, 0, nullptr);
+                d.rc = dev_run(d, msg, msg_len, sh[(size_t)i].lo, sh[(size_t)i].hi, rchunk, 0, nullptr,
+                               ctx->policy);
             });
         }
         for (auto& t : th) t.join();
@@ -369,7 +377,7 @@ int gpuhash_hash_range(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uin
     HIPCHK(hipSetDevice(d.ord));
     unsigned long long* dd = nullptr;
     if (hipMalloc(&dd, count * sizeof(uint64_t)) != hipSuccess) return GPUHASH_ENOMEM;
-    int rc = dev_run(d, msg, msg_len, lower, lower + count - 1, 0, 1, dd);
+    int rc = dev_run(d, msg, msg_len, lower, lower + count - 1, 0, 1, dd, ctx->policy);
     if (!rc && hipMemcpy(out, dd, count * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
         rc = GPUHASH_EHIP;
     hipFree(dd);

@@ -13,7 +13,12 @@
 
 using namespace gpuhash;
 
+static int g_policy = kLayoutAuto;
+
 extern "C" {
+
+// Layout policy used by every plan_* / hostcheck_* call below (plan.h LayoutPolicy).
+void hostcheck_set_layout_policy(int policy) { g_policy = policy; }
 
 struct gpuhash_plan_info {
     int J, C2, EX, d, q, s;
@@ -25,7 +30,7 @@ int gpuhash_plan_count(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_
                        uint32_t rchunk) {
     if (lower > upper) return -1;
     std::vector<Launch> v;
-    plan_range(msg, len, lower, upper, v, rchunk);
+    plan_range(msg, len, lower, upper, v, rchunk, g_policy);
     return (int)v.size();
 }
 
@@ -33,7 +38,7 @@ int gpuhash_plan_get(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t 
                      uint32_t rchunk, int idx, gpuhash_plan_info* out) {
     if (lower > upper || !out) return -1;
     std::vector<Launch> v;
-    plan_range(msg, len, lower, upper, v, rchunk);
+    plan_range(msg, len, lower, upper, v, rchunk, g_policy);
     if (idx < 0 || idx >= (int)v.size()) return -1;
     const Launch& l = v[(size_t)idx];
     const LaunchDesc& D = l.desc;
@@ -47,7 +52,7 @@ int gpuhash_plan_all(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t 
                      uint32_t rchunk, gpuhash_plan_info* out, int cap) {
     if (lower > upper) return -1;
     std::vector<Launch> v;
-    plan_range(msg, len, lower, upper, v, rchunk);
+    plan_range(msg, len, lower, upper, v, rchunk, g_policy);
     for (int i = 0; i < (int)v.size() && i < cap; i++) {
         const Launch& l = v[(size_t)i];
         const LaunchDesc& D = l.desc;
@@ -73,7 +78,7 @@ int gpuhash_shard(uint64_t msg_len, uint64_t lower, uint64_t upper, int n, uint6
 int hostcheck_desc_hash(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper,
                         uint32_t rchunk, int idx, uint64_t nonce, uint64_t* out) {
     std::vector<Launch> v;
-    plan_range(msg, len, lower, upper, v, rchunk);
+    plan_range(msg, len, lower, upper, v, rchunk, g_policy);
     if (idx < 0 || idx >= (int)v.size()) return -1;
     const Launch& l = v[(size_t)idx];
     const LaunchDesc& D = l.desc;

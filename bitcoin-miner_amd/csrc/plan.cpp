@@ -115,7 +115,8 @@ struct GroupLayout {
     uint64_t B;  // index of the block holding the last digit
 };
 
-GroupLayout layout_for(uint64_t m, int d) {
+// `span` = nonces of this digit group in the search (0 = unknown: assume a full group).
+GroupLayout layout_for(uint64_t m, int d, uint64_t span = 0, int policy = kLayoutAuto) {
     GroupLayout g{};
     g.d = d;
     uint64_t L = m + 1 + (uint64_t)d;
@@ -137,9 +138,18 @@ GroupLayout layout_for(uint64_t m, int d) {
     // at least 3 digits (>= 1000 lane values, rows stay full), move W_0's digits into the
     // loop so block B carries loop digits only (C2 = 2: uniform schedule, no per-nonce
     // schedule work); the lanes take the digits at the end of block B-1.
+    // A lane then covers R = 10^(4+q1) loop values, up to 10^8, so a narrow search fills
+    // only part of a 256-lane row: keep the classic layout (29-31 GH/s) when the expected
+    // row fill would make the uniform one (45 GH/s at full rows) slower.
     if (g.C2 && g.J == 1) {
         const int nb1 = d - 4 - g.q;  // digits in block B-1 and earlier
-        if (nb1 >= 3) {
+        bool fill_ok = policy != kLayoutClassic;
+        if (span && policy == kLayoutAuto) {
+            const uint64_t lanes = (span - 1) / pow10u(4 + g.q) + 1;  // lane values touched
+            const uint64_t rows = (lanes + kBlock - 1) / kBlock;
+            fill_ok = (double)lanes / (double)(rows * kBlock) >= 0.65;
+        }
+        if (nb1 >= 3 && fill_ok) {
             g.C2 = 2;
             g.q1 = g.q;
             g.q = 4 + g.q;
@@ -240,7 +250,7 @@ void build_launch(const uint8_t* msg, uint64_t m, const GroupLayout& g, uint64_t
 }  // namespace
 
 void plan_range(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper,
-                std::vector<Launch>& out, uint32_t rchunk_max) {
+                std::vector<Launch>& out, uint32_t rchunk_max, int policy) {
     const int dlo = num_digits(lower), dhi = num_digits(upper);
     for (int d = dlo; d <= dhi; d++) {
         uint64_t a = d == 1 ? 0 : pow10u(d - 1);
@@ -248,7 +258,7 @@ void plan_range(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper
         a = std::max(a, lower);
         b = std::min(b, upper);
         if (a > b) continue;
-        GroupLayout g = layout_for(len, d);
+        GroupLayout g = layout_for(len, d, b - a == UINT64_MAX ? 0 : b - a + 1, policy);
         const uint64_t U = pow10u(g.s + g.q);
         const uint64_t Hf = a / U, Hl = b / U;
         for (uint64_t H = Hf;; H++) {

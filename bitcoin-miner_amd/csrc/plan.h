@@ -83,10 +83,16 @@ static constexpr int kMaxLaunchDigits = 10;   // s + q <= 10  -> <= 10^10 nonces
 // C2 = 2 launches: s + q <= 12 still keeps rows * R = ceil(10^s / 256) * 10^q < 2^32
 static constexpr int kMaxLaunchDigitsU2 = 12;
 
+// Choice between the two J = 1 straddling layouts (plan.cpp layout_for):
+//   auto     C2 = 2 (uniform two-word loop) when the search fills >= 65% of its rows
+//   uniform  C2 = 2 whenever block B-1 holds >= 3 digits (tuning / parity tests)
+//   classic  never C2 = 2
+enum LayoutPolicy { kLayoutAuto = 0, kLayoutUniform = 1, kLayoutClassic = 2 };
+
 // Plans [lower, upper] (inclusive, lower <= upper) of `msg`.  `rchunk_max` caps the r
 // values per work item (0 = default).  Appends to `out`.
 void plan_range(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper,
-                std::vector<Launch>& out, uint32_t rchunk_max = 0);
+                std::vector<Launch>& out, uint32_t rchunk_max = 0, int policy = kLayoutAuto);
 
 struct Shard {
     uint64_t lo, hi;  // inclusive

@@ -35,10 +35,11 @@ GPUHASH_EHIP = -3
 GPUHASH_ETOOLONG = -4
 GPUHASH_ENOMEM = -5
 GPUHASH_MAX_MSG = 1 << 20
+LAYOUT_AUTO, LAYOUT_UNIFORM, LAYOUT_CLASSIC = 0, 1, 2
 
 # Every symbol include/gpuhash.h declares (tests check the .so exports all of them).
 EXPORTED = [
-    "gpuhash_open", "gpuhash_ndevices", "gpuhash_min", "gpuhash_min_ex",
+    "gpuhash_open", "gpuhash_ndevices", "gpuhash_set_layout_policy", "gpuhash_min", "gpuhash_min_ex",
     "gpuhash_hash_range", "gpuhash_hash_cpu", "gpuhash_last_stats", "gpuhash_last_launches",
     "gpuhash_close",
     "gpuhash_strerror", "gpuhash_version",
@@ -93,6 +94,8 @@ def _lib(path: str | None = None) -> ctypes.CDLL:
     lib.gpuhash_ndevices.restype = ctypes.c_int
     lib.gpuhash_min.argtypes = [vp, u8p, sz, u64, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]
     lib.gpuhash_min.restype = ctypes.c_int
+    lib.gpuhash_set_layout_policy.argtypes = [vp, ctypes.c_int]
+    lib.gpuhash_set_layout_policy.restype = ctypes.c_int
     lib.gpuhash_min_ex.argtypes = [vp, u8p, sz, u64, u64, ctypes.c_uint32,
                                    ctypes.POINTER(u64), ctypes.POINTER(u64)]
     lib.gpuhash_min_ex.restype = ctypes.c_int
@@ -137,6 +140,12 @@ class Engine:
     @property
     def ndevices(self) -> int:
         return self._lib.gpuhash_ndevices(self._ctx)
+
+    def set_layout_policy(self, policy: int) -> None:
+        """LAYOUT_AUTO / LAYOUT_UNIFORM / LAYOUT_CLASSIC (gpuhash_set_layout_policy)."""
+        rc = self._lib.gpuhash_set_layout_policy(self._ctx, policy)
+        if rc != GPUHASH_OK:
+            raise GpuHashError(rc, "gpuhash_set_layout_policy")
 
     def min(self, msg, lower: int, upper: int, rchunk: int = 0) -> tuple[int, int]:
         """argmin over inclusive [lower, upper] of (Hash(msg, n), n)."""

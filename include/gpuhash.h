@@ -63,7 +63,8 @@ typedef struct gpuhash_stats {
 typedef struct gpuhash_launch_record {
     int32_t device;   /* HIP ordinal                                                */
     int32_t J;        /* kernel variant: loop-word index in the final block (0..15) */
-    int32_t C2;       /* 1: lane digits spill into the previous block               */
+    int32_t C2;       /* 1: lane digits spill into the previous block; 2: and the   */
+                      /*    last block's W_0/W_1 are loop words (uniform schedule)  */
     int32_t EX;       /* 1: extra all-constant padding block                        */
     int32_t digits;   /* decimal digits of every nonce in the launch                */
     int32_t c;        /* 64-byte blocks holding nonce digits (1 or 2)               */
@@ -80,6 +81,17 @@ int gpuhash_open(const int *devices, int ndevices, gpuhash_ctx **out);
 
 /* Number of devices a context drives. */
 int gpuhash_ndevices(const gpuhash_ctx *ctx);
+
+/* Layout choice for nonces whose digits straddle two SHA blocks with 5-8 digits in the
+ * last one: AUTO (default) takes the uniform-schedule layout when the
+ * search fills its lane rows, UNIFORM always takes it, CLASSIC never.  Results are
+ * identical under every policy; only speed differs.  Exposed for tuning and so that
+ * parity tests can drive both kernels over small ranges.  Replaces nothing in the
+ * reference. */
+#define GPUHASH_LAYOUT_AUTO 0
+#define GPUHASH_LAYOUT_UNIFORM 1
+#define GPUHASH_LAYOUT_CLASSIC 2
+int gpuhash_set_layout_policy(gpuhash_ctx *ctx, int policy);
 
 /* argmin_{n in [lower, upper]} (Hash(msg, n), n) -> *out_hash, *out_nonce.
  * Replaces the miner loop of p1.pdf pp.12-14 (miner.go:15) and feeds

@@ -66,13 +66,16 @@ def test_hash_range_bit_exact(engine, oracle):
     (58, 10, 2, 1), (59, 10, 2, 1), (60, 10, 2, 1), (56, 12, 2, 1), (59, 12, 2, 1),  # two-word loop
     (120, 10, 1, 0), (54, 10, 1, 0), (119, 12, 1, 0),                                # K+W table
 ])
-def test_uniform_schedule_layouts(engine, oracle, mlen, d, c2, j):
+def test_uniform_schedule_layouts(engine, oracle, mlen, d, c2, j, request):
     """Layouts whose final block holds loop digits only (its schedule is built once per
     loop value: C2=1/J=0 from the k_ktab table, C2=2/J=1 in LDS): per-nonce parity over
     windows where the W_1 and W_0 loop digits roll over, and min parity."""
+    import gpuhash
     rng = random.Random(mlen * 100 + d)
     m = bytes(rng.randrange(32, 127) for _ in range(mlen))
     base = 10 ** (d - 1) + rng.randrange(10 ** (d - 2))
+    engine.set_layout_policy(gpuhash.LAYOUT_UNIFORM)  # small ranges would pick C2=1 under AUTO
+    request.addfinalizer(lambda: engine.set_layout_policy(gpuhash.LAYOUT_AUTO))
     engine.min(m, base, base + 1000)
     assert any(r["C2"] == c2 and r["J"] == j for r in engine.launches()), engine.launches()
     for lo in (base - base % 10 ** 4 - 700, base - base % 10 ** 8 - 3000, base + 12345):
@@ -82,6 +85,24 @@ def test_uniform_schedule_layouts(engine, oracle, mlen, d, c2, j):
         assert bad.size == 0, (mlen, d, lo, int(bad[0]) + lo if bad.size else None)
     for lo, hi in ((base, base + 2_000_000), (base - base % 10 ** 6 - 77, base - base % 10 ** 6 + 300_000)):
         assert engine.min(m, lo, hi) == oracle.min(m, lo, hi), (mlen, d, lo, hi)
+
+
+def test_layout_policies_agree(engine, request):
+    """The straddling J=1 digit groups under UNIFORM, CLASSIC and AUTO: same answers
+    (each is bit-exact against the oracle elsewhere; here at sizes past the oracle's)."""
+    import gpuhash
+    request.addfinalizer(lambda: engine.set_layout_policy(gpuhash.LAYOUT_AUTO))
+    for m, lo, n in ((b"y" * 59, 10 ** 11 + 12345, 3 * 10 ** 10), (M120[:58], 10 ** 9 + 7, 2 * 10 ** 9)):
+        got = {}
+        for pol in (gpuhash.LAYOUT_UNIFORM, gpuhash.LAYOUT_CLASSIC, gpuhash.LAYOUT_AUTO):
+            engine.set_layout_policy(pol)
+            got[pol] = engine.min(m, lo, lo + n)
+            got[(pol, "c2")] = {r["C2"] for r in engine.launches()}
+        assert got[gpuhash.LAYOUT_UNIFORM] == got[gpuhash.LAYOUT_CLASSIC] == got[gpuhash.LAYOUT_AUTO]
+        assert 2 in got[(gpuhash.LAYOUT_UNIFORM, "c2")] and 2 not in got[(gpuhash.LAYOUT_CLASSIC, "c2")]
+        assert gpuhash.Hash(m, got[gpuhash.LAYOUT_AUTO][1]) == got[gpuhash.LAYOUT_AUTO][0]
+    with pytest.raises(gpuhash.GpuHashError):
+        engine.set_layout_policy(7)
 
 
 def test_ktab_several_digit_groups_in_one_call(engine, oracle):

@@ -39,7 +39,12 @@ def hc():
     lib.hostcheck_desc_hash.argtypes = [cp, u64, u64, u64, u32, ctypes.c_int, u64, ctypes.POINTER(u64)]
     lib.gpuhash_shard.argtypes = [u64, u64, u64, ctypes.c_int, ctypes.POINTER(u64),
                                   ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_int)]
+    lib.hostcheck_set_layout_policy.argtypes = [ctypes.c_int]
+    lib.hostcheck_set_layout_policy(AUTO)
     return lib
+
+
+AUTO, UNIFORM, CLASSIC = 0, 1, 2
 
 
 def plan(hc, m, a, b, rchunk=0):
@@ -78,7 +83,9 @@ def test_plan_tiles_range_and_layouts_are_legal(hc):
             assert l.nrchunks * l.rchunk >= l.R
 
 
-def test_descriptor_replay_matches_oracle(hc, oracle):
+@pytest.mark.parametrize("policy", [AUTO, UNIFORM])
+def test_descriptor_replay_matches_oracle(hc, oracle, policy):
+    hc.hostcheck_set_layout_policy(policy)
     rng = random.Random(5)
     seen = set()
     for _ in range(1500):
@@ -92,8 +99,30 @@ def test_descriptor_replay_matches_oracle(hc, oracle):
             seen.add((l.J, l.C2, l.EX))
             for n in {l.lo, l.hi, rng.randrange(l.lo, l.hi + 1)}:
                 assert desc_hash(hc, m, a, b, i, n) == oracle.hash(m, n), (m, a, b, i, n)
+    hc.hostcheck_set_layout_policy(AUTO)
     # every one of the 20 reachable (J, C2, EX) variants was exercised
-    assert len(seen) == 20, sorted(seen)
+    if policy == UNIFORM:
+        assert len(seen) == 20, sorted(seen)
+    else:
+        assert len(seen) >= 19, sorted(seen)
+
+
+def test_layout_policy_for_straddling_j1(hc):
+    """m = 59, d = 12: digits 60..71, 4 in block 0 and 8 in block 1 (W_0 + W_1).  The
+    uniform two-word loop has R = 10^8 loop values per lane, so AUTO takes it only when
+    the search fills >= 65% of its 256-lane rows; CLASSIC never, UNIFORM always."""
+    m = b"y" * 59
+    lo = 10 ** 11
+    narrow, wide = (lo, lo + 10 ** 9), (lo, lo + 5 * 10 ** 11)  # both stay at d = 12
+    pick = lambda a, b: {(l.J, l.C2) for l in plan(hc, m, a, b)}
+    assert pick(*narrow) == {(1, 1)} and pick(*wide) == {(1, 2)}
+    try:
+        hc.hostcheck_set_layout_policy(UNIFORM)
+        assert pick(*narrow) == {(1, 2)}
+        hc.hostcheck_set_layout_policy(CLASSIC)
+        assert pick(*wide) == {(1, 1)}
+    finally:
+        hc.hostcheck_set_layout_policy(AUTO)
 
 
 @pytest.mark.parametrize("mlen", [0, 8, 44, 45, 53, 54, 55, 56, 63, 64, 110, 119, 120, 127, 128, 180])
