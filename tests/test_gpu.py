@@ -135,6 +135,14 @@ def test_min_matches_oracle_random(engine, oracle):
         assert engine.min(m, lo, hi) == oracle.min(m, lo, hi), (m, lo, hi)
 
 
+@pytest.mark.parametrize("mlen", [1000, 1300])
+def test_long_messages(engine, oracle, mlen):
+    m = bytes((i * 131 + 7) % 256 for i in range(mlen))
+    for lo in (0, 999_990_000, 10 ** 12 - 5000):
+        assert engine.min(m, lo, lo + 300_000) == oracle.min(m, lo, lo + 300_000)
+        assert (engine.hash_range(m, lo, 3000) == oracle.hash_range(m, lo, 3000)).all()
+
+
 def test_single_nonce_ranges(engine, oracle):
     rng = random.Random(1)
     for n in [0, 1, 9, 10, 99, 100, 12345, 10 ** 9 - 1, 10 ** 9, 2 ** 32 - 1, 10 ** 19, U64 - 1, U64] + \

@@ -137,6 +137,20 @@ def test_every_digit_count_and_message_length(hc, oracle, mlen):
                     assert desc_hash(hc, m, a, b, i, n) == oracle.hash(m, n)
 
 
+@pytest.mark.parametrize("mlen", [1000, 1299, 1300, 4093])
+def test_long_messages(hc, oracle, mlen):
+    # the LSP packet budget caps real messages near 1.3 KB; the host
+    # midstate covers every block before the digits
+    m = bytes((i * 131 + 7) % 256 for i in range(mlen))
+    for d in (1, 9, 10, 12, 20):
+        lo = 0 if d == 1 else 10 ** (d - 1)
+        hi = min(10 ** d - 1, U64)
+        a, b = lo, min(hi, lo + 99_999)
+        for i, l in enumerate(plan(hc, m, a, b)):
+            for n in (l.lo, l.hi):
+                assert desc_hash(hc, m, a, b, i, n) == oracle.hash(m, n)
+
+
 def test_wide_ranges_plan(hc):
     for a, b in [(0, (1 << 40) - 1), (0, (1 << 32) - 1), (U64 - 10 ** 12, U64)]:
         p = plan(hc, b"bradfitz", a, b)
