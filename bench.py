@@ -107,6 +107,19 @@ def pmc_traffic(key) -> float | None:
         return None
 
 
+def pmc_issued(key) -> float | None:
+    """VALU wave-instructions per launch of the dominant kernel from the committed PMC
+    summary (SQ_INSTS_VALU, its own --pmc pass); x64 lanes / nonces = issued
+    lane-instructions per nonce, the hardware-counted work behind `achieved`."""
+    path = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        return t["kernels"][f"k_scan<{key[0]}, {int(key[1])}, {str(bool(key[2])).lower()}, 0>"]["per_launch"]["SQ_INSTS_VALU"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -187,6 +200,8 @@ def main() -> None:
     ops_per_launch = dom["nonces"] / dom["n"] * OPS_PER_BLOCK * dom["c"]
     achieved_T = ops_per_launch / (avg_ms * 1e-3) / 1e12
     kernel_ghs = dom["nonces"] / (dom["ms"] * 1e-3) / 1e9
+    insts = pmc_issued(key) if args.config == "2" else None  # PMC pass was config 2
+    issued_per_nonce = insts * 64 / (dom["nonces"] / dom["n"]) if insts else None
 
     if rank == 0:
         total = per_gpu * world * args.steps
@@ -220,6 +235,14 @@ def main() -> None:
                 "nonces_per_launch": dom["nonces"] / dom["n"],
                 "ops_per_nonce": OPS_PER_BLOCK * dom["c"],
                 "kernel_GHs": round(kernel_ghs, 4),
+                # hardware-counted view (bounded by the issue rate, not by the algorithm):
+                # SQ_INSTS_VALU x 64 / nonce from the committed PMC pass, times this run's rate
+                "issued_lane_instr_per_nonce": round(issued_per_nonce, 1) if issued_per_nonce else None,
+                "issued_T": round(kernel_ghs * issued_per_nonce / 1e3, 3) if issued_per_nonce else None,
+                "issued_frac": round(kernel_ghs * issued_per_nonce / 1e3 / VALU_PEAK_T, 4) if issued_per_nonce else None,
+                # the guide's SIMD-32 nominal (2-cycle wave64 issue) rate: reachable only by
+                # streams without v_alignbit/v_add3, so not the bound here
+                "simd32_nominal_peak": round(VALU_PEAK_T * 2, 3),
             },
         }
         if world == 1 and not args.no_cpu_baseline and args.config == "2":

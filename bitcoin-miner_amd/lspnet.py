@@ -5,7 +5,8 @@ Mirrors src/github.com/cmu440/lspnet of the reference:
                    connection so drops can be injected per role
   * conn.go:34-113 Read / ReadFromUDP / Write / WriteToUDP, each applying the role's
                    read or write drop percentage (dropIt, conn.go:115-117)
-  * staff.go:27-58 Set{Client,Server}{Read,Write}DropPercent, EnableDebugLogs
+  * staff.go:14-48 Set{Client,Server}{Read,Write}DropPercent, ResetDropPercent,
+                   EnableDebugLogs
 Separate processes (BASELINE config 5) take the same knobs from the environment:
 LSPNET_CLIENT_READ_DROP, LSPNET_CLIENT_WRITE_DROP, LSPNET_SERVER_READ_DROP,
 LSPNET_SERVER_WRITE_DROP (percent, 0-100).
@@ -52,6 +53,12 @@ def SetReadDropPercent(p: int) -> None:
 def SetWriteDropPercent(p: int) -> None:
     SetClientWriteDropPercent(p)
     SetServerWriteDropPercent(p)
+
+
+def ResetDropPercent() -> None:
+    """staff.go:44-48: all four drop percentages back to 0."""
+    SetReadDropPercent(0)
+    SetWriteDropPercent(0)
 
 
 def EnableDebugLogs(on: bool) -> None:
