@@ -7,7 +7,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <new>
 #include <string>
 #include <thread>
 #include <vector>
@@ -18,6 +20,10 @@
 using namespace gpuhash;
 
 namespace {
+
+// Nonces per device in one slice of a search (gpuhash_min_ex): 2^38 is ~8 s of work on
+// one MI355X at config-2 rates.
+constexpr uint64_t kSlicePerDevice = 1ull << 38;
 
 struct Dev {
     int ord = -1;
@@ -290,7 +296,8 @@ int gpuhash_open(const int* devices, int ndevices, gpuhash_ctx** out) {
         if (hipGetDeviceProperties(&p, o) != hipSuccess) return GPUHASH_ENODEV;
         if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0) return GPUHASH_ENODEV;
     }
-    auto* ctx = new gpuhash_ctx();
+    auto* ctx = new (std::nothrow) gpuhash_ctx();
+    if (!ctx) return GPUHASH_ENOMEM;
     ctx->devs.resize(ords.size());
     for (size_t i = 0; i < ords.size(); i++) {
         int rc = dev_init(ctx->devs[i], ords[i]);
@@ -312,12 +319,11 @@ int gpuhash_set_layout_policy(gpuhash_ctx* ctx, int policy) {
     return GPUHASH_OK;
 }
 
-int gpuhash_min_ex(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uint64_t lower,
-                   uint64_t upper, uint32_t rchunk, uint64_t* out_hash, uint64_t* out_nonce) {
-    if (!ctx || !out_hash || !out_nonce || (msg_len && !msg)) return GPUHASH_EINVAL;
-    if (lower > upper) return GPUHASH_EINVAL;
-    if (msg_len > GPUHASH_MAX_MSG) return GPUHASH_ETOOLONG;
-    auto t0 = std::chrono::steady_clock::now();
+// One slice of a search: sharded over the context's devices, each shard on its own
+// host thread + stream, 16-byte host argmin.  Accumulates into st / ctx->recs.
+static int run_slice(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uint64_t lower,
+                     uint64_t upper, uint32_t rchunk, uint64_t& bh, uint64_t& bn, bool& any,
+                     gpuhash_stats& st) {
     const int n = (int)ctx->devs.size();
     std::vector<Shard> sh = shard_range(msg_len, lower, upper, n);
     for (auto& d : ctx->devs) { d.used = false; d.rc = GPUHASH_OK; d.kernel_ms = 0; d.launches = 0; }
@@ -329,16 +335,17 @@ int gpuhash_min_ex(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uint64_
             if (sh[(size_t)i].empty) continue;
             th.emplace_back([&, i] {
                 Dev& d = ctx->devs[(size_t)i];
-                d.rc = dev_run(d, msg, msg_len, sh[(size_t)i].lo, sh[(size_t)i].hi, rchunk, 0, nullptr,
-                               ctx->policy);
+                try {
+                    d.rc = dev_run(d, msg, msg_len, sh[(size_t)i].lo, sh[(size_t)i].hi, rchunk, 0, nullptr,
+                                   ctx->policy);
+                } catch (const std::bad_alloc&) {
+                    d.used = true;
+                    d.rc = GPUHASH_ENOMEM;
+                }
             });
         }
         for (auto& t : th) t.join();
     }
-    uint64_t bh = ~0ull, bn = ~0ull;
-    gpuhash_stats st{};
-    bool any = false;
-    ctx->recs.clear();
     for (auto& d : ctx->devs) {
         if (!d.used) continue;
         if (d.rc) return d.rc;
@@ -346,18 +353,65 @@ int gpuhash_min_ex(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uint64_
         if (!any || d.best_h < bh || (d.best_h == bh && d.best_n < bn)) { bh = d.best_h; bn = d.best_n; }
         any = true;
         ctx->recs.insert(ctx->recs.end(), d.recs.begin(), d.recs.end());
-        st.ndevices++;
         st.launches += d.launches;
         st.kernel_ms += d.kernel_ms;
-        st.max_dev_kernel_ms = std::max(st.max_dev_kernel_ms, d.kernel_ms);
     }
-    uint64_t span = upper - lower;
-    st.nonces = span == ~0ull ? ~0ull : span + 1;
-    st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    ctx->last = st;
-    *out_hash = bh;
-    *out_nonce = bn;
     return GPUHASH_OK;
+}
+
+int gpuhash_min_ex(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uint64_t lower,
+                   uint64_t upper, uint32_t rchunk, uint64_t* out_hash, uint64_t* out_nonce) {
+    if (!ctx || !out_hash || !out_nonce || (msg_len && !msg)) return GPUHASH_EINVAL;
+    if (lower > upper) return GPUHASH_EINVAL;
+    if (msg_len > GPUHASH_MAX_MSG) return GPUHASH_ETOOLONG;
+    try {
+        auto t0 = std::chrono::steady_clock::now();
+        const uint64_t n = ctx->devs.size();
+        // Searches longer than kSlicePerDevice nonces per device run as consecutive
+        // slices: every launch descriptor covers <= 10^10-10^12 nonces (plan.h), so one
+        // slice's plan stays a few hundred descriptors, whatever the span (a 2^64 range
+        // would otherwise plan ~10^9 of them).  A slice is ~8 s of GPU work, so the
+        // per-slice sync and 16-byte merge cost nothing measurable.
+        // GPUHASH_SLICE_NONCES overrides the per-device slice (tests use it to exercise
+        // the slice loop, including its end at 2^64-1, on oracle-sized ranges).
+        uint64_t per_dev = kSlicePerDevice;
+        if (const char* e = std::getenv("GPUHASH_SLICE_NONCES")) {
+            const unsigned long long v = std::strtoull(e, nullptr, 10);
+            if (v > 0) per_dev = v;
+        }
+        const uint64_t slice = per_dev > ~0ull / n ? ~0ull : per_dev * n;
+        uint64_t bh = ~0ull, bn = ~0ull;
+        bool any = false;
+        gpuhash_stats st{};
+        ctx->recs.clear();
+        uint32_t ndev_used = 0;
+        for (uint64_t lo = lower;;) {
+            const uint64_t hi = upper - lo < slice ? upper : lo + (slice - 1);
+            int rc = run_slice(ctx, msg, msg_len, lo, hi, rchunk, bh, bn, any, st);
+            if (rc) return rc;
+            double slice_max = 0;
+            uint32_t used = 0;
+            for (auto& d : ctx->devs) {
+                if (!d.used) continue;
+                slice_max = std::max(slice_max, d.kernel_ms);
+                used++;
+            }
+            st.max_dev_kernel_ms += slice_max;  // devices run a slice concurrently
+            ndev_used = std::max(ndev_used, used);
+            if (hi == upper) break;
+            lo = hi + 1;
+        }
+        st.ndevices = ndev_used;
+        uint64_t span = upper - lower;
+        st.nonces = span == ~0ull ? ~0ull : span + 1;
+        st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        ctx->last = st;
+        *out_hash = bh;
+        *out_nonce = bn;
+        return GPUHASH_OK;
+    } catch (const std::bad_alloc&) {
+        return GPUHASH_ENOMEM;
+    }
 }
 
 int gpuhash_min(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uint64_t lower,
@@ -377,7 +431,12 @@ int gpuhash_hash_range(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uin
     HIPCHK(hipSetDevice(d.ord));
     unsigned long long* dd = nullptr;
     if (hipMalloc(&dd, count * sizeof(uint64_t)) != hipSuccess) return GPUHASH_ENOMEM;
-    int rc = dev_run(d, msg, msg_len, lower, lower + count - 1, 0, 1, dd, ctx->policy);
+    int rc;
+    try {
+        rc = dev_run(d, msg, msg_len, lower, lower + count - 1, 0, 1, dd, ctx->policy);
+    } catch (const std::bad_alloc&) {
+        rc = GPUHASH_ENOMEM;
+    }
     if (!rc && hipMemcpy(out, dd, count * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
         rc = GPUHASH_EHIP;
     hipFree(dd);

@@ -97,7 +97,9 @@ int gpuhash_set_layout_policy(gpuhash_ctx *ctx, int policy);
  * Replaces the miner loop of p1.pdf pp.12-14 (miner.go:15) and feeds
  * bitcoin.NewResult(hash, nonce) (message.go:36-42).  msg is read during the call
  * only (cgo pointer rules); the range is split statically over the context's devices
- * (one host thread + one stream each), reduced on the host.  Blocking. */
+ * (one host thread + one stream each), reduced on the host.  Blocking.  Any span is
+ * accepted, up to the full [0, 2^64-1]: spans over 2^38 nonces per device run as
+ * consecutive slices (env GPUHASH_SLICE_NONCES overrides the per-device slice). */
 int gpuhash_min(gpuhash_ctx *ctx, const uint8_t *msg, size_t msg_len, uint64_t lower,
                 uint64_t upper, uint64_t *out_hash, uint64_t *out_nonce);
 

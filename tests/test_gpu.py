@@ -227,3 +227,33 @@ def test_native_library_is_the_one_loaded(engine):
     import gpuhash
     maps = open("/proc/self/maps").read()
     assert gpuhash.LIB_PATH in maps
+
+
+@pytest.mark.parametrize("slice_nonces", [1, 999, 250000])
+def test_sliced_search_matches_oracle(engine, oracle, monkeypatch, slice_nonces):
+    """Searches longer than one slice run as consecutive slices merged on the host
+    (gpuhash_min_ex).  A small GPUHASH_SLICE_NONCES drives that loop over oracle-sized
+    ranges: across digit-count boundaries, ending exactly at 2^64-1 (the loop's overflow
+    edge), and with the minimum in a late slice."""
+    monkeypatch.setenv("GPUHASH_SLICE_NONCES", str(slice_nonces))
+    cases = [(b"bradfitz", 999_000, 1_001_000), (M120, 10 ** 9 - 700, 10 ** 9 + 700),
+             (b"edge", U64 - 600_000, U64)]
+    if slice_nonces == 1:
+        cases = [(b"bradfitz", 0, 60), (b"edge", U64 - 40, U64)]
+    for m, lo, hi in cases:
+        assert engine.min(m, lo, hi) == oracle.min(m, lo, hi), (m, lo, hi)
+        st = engine.stats()
+        assert st["nonces"] == hi - lo + 1
+        assert st["launches"] >= (hi - lo + 1 + slice_nonces - 1) // slice_nonces
+
+
+def test_top_of_u64_range_in_slices(engine, monkeypatch):
+    """Unsliced, a span this close to 2^64 would plan one descriptor per 10^10 nonces
+    over the whole call (a full [0, 2^64-1] search threw std::bad_alloc through the C
+    ABI).  The top 3 slices of the range run 20-digit plans and end the slice loop at
+    2^64-1; the winner re-hashes to the reported hash on the host."""
+    import gpuhash
+    monkeypatch.setenv("GPUHASH_SLICE_NONCES", str(1 << 20))
+    lo = U64 - 3 * (1 << 20) + 1
+    h, n = engine.min(b"bradfitz", lo, U64)
+    assert lo <= n <= U64 and gpuhash.Hash(b"bradfitz", n) == h
