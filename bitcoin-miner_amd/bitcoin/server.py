@@ -46,12 +46,28 @@ class Job:
 
 @dataclass
 class Request:
+    """One client request.  Jobs are cut lazily from [next_lo, upper] (a request may span
+    all of [0, 2^64-1], i.e. 2^30 jobs, so they are never materialised); jobs of lost
+    miners wait in `requeued` and go out first."""
     req_id: int
     client: int
     data: str
-    pending: collections.deque = field(default_factory=collections.deque)
+    next_lo: int = 0
+    upper: int = -1       # next_lo > upper: nothing left to cut
+    requeued: collections.deque = field(default_factory=collections.deque)
     inflight: int = 0
     best: tuple | None = None
+
+    def has_pending(self) -> bool:
+        return bool(self.requeued) or self.next_lo <= self.upper
+
+    def pop_job(self, size: int) -> Job:
+        if self.requeued:
+            return self.requeued.popleft()
+        lo = self.next_lo
+        hi = min(self.upper, lo + size - 1)
+        self.next_lo = hi + 1
+        return Job(self.req_id, lo, hi)
 
 
 def split_jobs(req_id: int, lower: int, upper: int, size: int):
@@ -82,23 +98,21 @@ class Scheduler:
 
     def add_request(self, client: int, data: str, lower: int, upper: int) -> int:
         rid = next(self._ids)
-        r = Request(rid, client, data)
-        if lower <= upper:
-            r.pending.extend(split_jobs(rid, lower, upper, self.job_size))
+        r = Request(rid, client, data, next_lo=lower, upper=upper)
         self.requests[rid] = r
         return rid
 
     def next_assignment(self):
         """(miner, job, data) for the next dispatch, or None."""
         while self.idle:
-            cands = [r for r in self.requests.values() if r.pending]
+            cands = [r for r in self.requests.values() if r.has_pending()]
             if not cands:
                 return None
             r = min(cands, key=lambda x: (x.inflight, x.req_id))
             miner = self.idle.popleft()
             if miner not in self.miners:
                 continue
-            job = r.pending.popleft()
+            job = r.pop_job(self.job_size)
             r.inflight += 1
             self.miners[miner] = job
             return miner, job, r.data
@@ -117,7 +131,7 @@ class Scheduler:
         r.inflight -= 1
         if r.best is None or (h, n) < r.best:
             r.best = (h, n)
-        if not r.pending and r.inflight == 0:
+        if not r.has_pending() and r.inflight == 0:
             del self.requests[r.req_id]
             return r.client, r.best
         return None
@@ -135,7 +149,7 @@ class Scheduler:
             if job is not None and job.req_id in self.requests:
                 r = self.requests[job.req_id]
                 r.inflight -= 1
-                r.pending.appendleft(job)
+                r.requeued.appendleft(job)
                 note += f"; job [{job.lower}, {job.upper}] of request {job.req_id} requeued"
         dropped = [rid for rid, r in self.requests.items() if r.client == conn]
         for rid in dropped:

@@ -117,6 +117,29 @@ def test_scheduler_drops_lost_client_and_ignores_late_results():
     assert s.next_assignment() is None
 
 
+def test_full_u64_request_cuts_jobs_lazily():
+    # [0, 2^64-1] is 2^30 jobs of 2^34: the scheduler must not materialise them
+    import time
+    s = bserver.Scheduler()
+    t = time.time()
+    rid = s.add_request(client=100, data="a", lower=0, upper=(1 << 64) - 1)
+    assert time.time() - t < 0.1
+    s.add_miner(1)
+    s.add_miner(2)
+    (m1, j1, _), (m2, j2, _) = s.next_assignment(), s.next_assignment()
+    assert (j1.lower, j1.upper, j2.lower) == (0, (1 << 34) - 1, 1 << 34)
+    s.lost(m1)  # the lost job goes out again before any new one
+    s.add_miner(3)
+    _, j3, _ = s.next_assignment()
+    assert (j3.lower, j3.upper) == (j1.lower, j1.upper)
+    r = s.requests[rid]
+    r.next_lo = (1 << 64) - 10  # fast-forward to the top of the range
+    s.result(m2, 9, 9)
+    _, j4, _ = s.next_assignment()
+    assert (j4.lower, j4.upper) == ((1 << 64) - 10, (1 << 64) - 1)
+    assert not r.has_pending()
+
+
 def test_merge_is_lexicographic():
     s = bserver.Scheduler(job_size=5)
     s.add_request(client=100, data="a", lower=0, upper=9)
