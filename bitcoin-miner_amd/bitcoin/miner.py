@@ -38,10 +38,15 @@ def run(hostport: str, engine=None, params=None, on_client=None) -> int:
     try:
         c.Write(marshal(NewJoin()))
         while True:
-            m = unmarshal(c.Read())
-            if m.Type != MsgType.Request:
+            try:
+                m = unmarshal(c.Read())
+            except (ValueError, KeyError):
+                continue  # not a Message: ignore, like the server does
+            if m.Type != MsgType.Request or m.Lower > m.Upper:
                 continue
             # was: for n := m.Lower; n <= m.Upper; n++ { h := bitcoin.Hash(m.Data, n) ... }
+            # an engine error (no device, HIP failure) propagates: the miner exits and
+            # the server requeues the job on another miner (p1.pdf p.15)
             h, n = engine.min(m.Data, m.Lower, m.Upper)
             c.Write(marshal(NewResult(h, n)))
             jobs += 1
