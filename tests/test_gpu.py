@@ -203,6 +203,18 @@ def test_multi_device_sharding_and_host_argmin(engine, oracle):
         assert multi.min(b"bradfitz", 0, 9999) == oracle.min(b"bradfitz", 0, 9999)
 
 
+def test_multi_device_sliced(engine, oracle, monkeypatch):
+    """Slices (gpuhash_min_ex) over several devices: each slice is sharded over the 3
+    entries and merged into the running argmin."""
+    import gpuhash
+    monkeypatch.setenv("GPUHASH_SLICE_NONCES", "3000")
+    with gpuhash.Engine([0, 0, 0]) as multi:
+        for m, lo, hi in [(b"bradfitz", 0, 99_999), (M120[:45], 9_999_990_000, 10_000_020_000),
+                          (b"edge", U64 - 50_000, U64)]:
+            assert multi.min(m, lo, hi) == oracle.min(m, lo, hi), (m, lo, hi)
+            assert multi.stats()["nonces"] == hi - lo + 1
+
+
 def test_plain_c_client_through_the_abi(oracle):
     """gpuhash_cli: a C process with no Python/torch, making the cgo binding's calls."""
     import os
