@@ -90,3 +90,26 @@ def test_tie_rule_lowest_nonce():
 def test_lower_gt_upper_is_error(oracle):
     with pytest.raises(ValueError):
         oracle.min(b"x", 5, 4)
+
+
+# FIPS 180-4 / NIST CSRC example digests for SHA-256 (independent of hashlib): pins the
+# oracle's compression function itself, not just its agreement with OpenSSL.
+FIPS_VECTORS = [
+    (b"", "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"),
+    (b"abc", "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"),
+    (b"abcdbcdecdefdefgefghfghighijhijkijkljklmklmnlmnomnopnopq",
+     "248d6a61d20638b8e5c026930c3e6039a33ce45964ff2167f6ecedd419db06c1"),
+    (b"abcdefghbcdefghicdefghijdefghijkefghijklfghijklmghijklmnhijklmnoijklmnopjklmnopqklmnopqr"
+     b"lmnopqrsmnopqrstnopqrstu",
+     "cf5b16a778af8380036ce59e7b0492370b249b11e8f07a51afac45037afee9d1"),
+    (b"a" * 1_000_000, "cdc76e5c9914fb9281a1c7e284d73e67f1809a48a497200e046d39ccc7112cd0"),
+]
+
+
+@pytest.mark.parametrize("data,digest", FIPS_VECTORS, ids=["empty", "abc", "448bit", "896bit", "million_a"])
+def test_c_sha256_fips_vectors(oracle, data, digest):
+    import ctypes
+    out = (ctypes.c_uint32 * 8)()
+    oracle.lib.oracle_sha256.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p]
+    oracle.lib.oracle_sha256(data, len(data), out)
+    assert "".join(f"{w:08x}" for w in out) == digest

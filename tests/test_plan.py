@@ -15,7 +15,8 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIBDIR = os.path.join(ROOT, "bitcoin-miner_amd", "lib")
-HC = os.path.join(LIBDIR, "libgpuhash_hostcheck.so")
+# tests/test_sanitizers.py reruns this module against the ASan/UBSan build
+HC = os.environ.get("GPUHASH_HOSTCHECK_LIB") or os.path.join(LIBDIR, "libgpuhash_hostcheck.so")
 U64 = (1 << 64) - 1
 u64 = ctypes.c_uint64
 
@@ -30,7 +31,7 @@ class Info(ctypes.Structure):
 def hc():
     if not os.path.exists(HC):
         subprocess.check_call(["make", "-C", os.path.join(ROOT, "bitcoin-miner_amd"),
-                               "lib/libgpuhash_hostcheck.so"])
+                               os.path.relpath(HC, os.path.join(ROOT, "bitcoin-miner_amd"))])
     lib = ctypes.CDLL(HC)
     cp, u32 = ctypes.c_char_p, ctypes.c_uint32
     lib.gpuhash_plan_count.argtypes = [cp, u64, u64, u64, u32]
