@@ -6,8 +6,9 @@ The restatement keeps the Go test's client count, message count, window size, Ep
 drop pattern and assertions, and drives `bitcoin-miner_amd/lsp` through the same API
 (NewServer/NewClient/Read/Write/CloseConn/Close and the lspnet drop knobs of staff.go).
 
-Time is scaled. Tests that need epochs to pass run with EpochMillis / EPOCH_DIV, floored
-at MIN_EPOCH_MS, and their time limits (maxEpochs x EpochMillis) scale with it. Tests that
+Time is scaled. Tests that need epochs to pass run with EpochMillis / EPOCH_DIV (the
+500-message lsp4 tests: / EPOCH_DIV_BULK), floored at MIN_EPOCH_MS, and their time limits
+(maxEpochs x EpochMillis) scale with it. Tests that
 must finish WITHOUT any epoch (TestBasic*, TestSendReceive*) keep their full epochs and
 time limits, so a message that needed a resend would still fail them.
 
@@ -36,12 +37,19 @@ EPOCH_DIV = 5
 MIN_EPOCH_MS = 100
 
 
-def scaled(epoch_ms: int) -> int:
-    return max(MIN_EPOCH_MS, epoch_ms // EPOCH_DIV) if epoch_ms > MIN_EPOCH_MS else epoch_ms
+# The 500-message lsp4 tests must move 5 x 500 window-1 round trips while the network is
+# on for 2 epochs; a Python endpoint under a loaded CPU needs more than 1/5 of the Go
+# test's 4 s for that, so those keep half their epoch length.
+EPOCH_DIV_BULK = 2
 
 
-def P(limit: int, millis: int, window: int, scale: bool = True) -> lsp.Params:
-    return lsp.Params(EpochLimit=limit, EpochMillis=scaled(millis) if scale else millis, WindowSize=window)
+def scaled(epoch_ms: int, div: int = EPOCH_DIV) -> int:
+    return max(MIN_EPOCH_MS, epoch_ms // div) if epoch_ms > MIN_EPOCH_MS else epoch_ms
+
+
+def P(limit: int, millis: int, window: int, scale: bool = True, div: int = EPOCH_DIV) -> lsp.Params:
+    return lsp.Params(EpochLimit=limit, EpochMillis=scaled(millis, div) if scale else millis,
+                      WindowSize=window)
 
 
 @pytest.fixture(autouse=True)
@@ -717,7 +725,8 @@ class SyncSystem:
 def test_lsp4_sync(name, nc, nmsgs, mode, params, max_epochs):
     # "fastclose" moves data both ways like RoundTrip, but issues the server's Close while
     # the network is still off (lsp4_test.go:395-397)
-    ts = SyncSystem(nc, nmsgs, mode, P(*params), max_epochs)
+    div = EPOCH_DIV_BULK if nmsgs >= 500 else EPOCH_DIV
+    ts = SyncSystem(nc, nmsgs, mode, P(*params, div=div), max_epochs)
     try:
         ts.master()
     finally:
