@@ -120,6 +120,57 @@ def pmc_issued(key) -> float | None:
         return None
 
 
+def main_inproc(args) -> None:
+    """All devices in ONE process: each step is one gpuhash_min over the union of the
+    per-GPU windows of ranks 0..N-1 (config 2/4: [0, N*per_gpu), weak scaling; config 3:
+    the same two windows split over N devices, strong scaling)."""
+    import gpuhash
+    devs = None if args.inproc == "all" else [int(x) for x in args.inproc.split(",")]
+    eng = gpuhash.Engine(devs)
+    n = eng.ndevices
+    cfg = CONFIGS[args.config]
+    msg = cfg["msg"]
+    wins = sorted({w for r in range(n) for w in cfg["windows"](r)})
+    merged = []
+    for lo, hi in wins:  # contiguous per-rank windows merge into one call
+        if merged and merged[-1][1] + 1 == lo:
+            merged[-1] = (merged[-1][0], hi)
+        else:
+            merged.append((lo, hi))
+    total_per_step = sum(hi - lo + 1 for lo, hi in merged)
+
+    def step(recs=None):
+        from gpuhash.dist import merge_min
+        parts = []
+        for lo, hi in merged:
+            parts.append(eng.min(msg, lo, hi))
+            if recs is not None:
+                recs.extend(eng.launches())
+        return merge_min(parts)
+
+    for _ in range(args.warmup):
+        step()
+    recs = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step(recs)
+    dt = time.perf_counter() - t0
+    value = total_per_step * args.steps / dt / 1e9
+    out = {
+        "metric": METRIC, "value": round(value, 4), "unit": "GH/s", "n_gpus": n,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "strong" if args.config == "3" else "weak",
+        "vs_baseline": None, "dtype": "u32", "data": "synthetic (the nonce space itself; fixed message)",
+        "config": {"workload": cfg["desc"] + " -- in-process, one gpuhash context over all devices",
+                   "msg_len": len(msg), "ranges": [list(w) for w in merged],
+                   "parallelism": f"inproc{n}", "devices": devs or "all"},
+        "per_gpu_GHs": round(value / n, 4), "result": list(res),
+        "launches_per_step": len(recs) // max(args.steps, 1),
+    }
+    print(json.dumps(out), flush=True)
+    eng.close()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -128,7 +179,14 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--config", default="2", choices=sorted(CONFIGS))
+    ap.add_argument("--inproc", default=None, metavar="DEVICES",
+                    help="one process drives these HIP devices (comma list or 'all') through "
+                         "one gpuhash context: static cost-balanced shards, one host thread + "
+                         "stream per device, 16-byte host argmin (SURVEY 8(e)); not used by "
+                         "the torchrun path")
     args = ap.parse_args()
+    if args.inproc is not None:
+        return main_inproc(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -2,7 +2,7 @@
 # tools/gpu_session.sh STEP... -- runs GPU steps on the gpurun box, each under its own
 # time limit, logging to gpurun_out/.  A plain failure (exit 1, e.g. a failing test)
 # lets the next step run; a fault, abort, segfault, time limit or kill stops the session.
-# Steps: valu | go | test | bench | prof | pmc | scale
+# Steps: valu | go | test | smoke | bench | bench3 | bench4 | dist2 | inproc | latency | prof | pmc | sweep | sys5
 set -u
 cd "$(dirname "$0")/.."
 OUT=gpurun_out
@@ -35,6 +35,9 @@ for step in "$@"; do
         smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 300 python -u bench.py --steps 10 --warmup 2 ;;
         dist2) run dist2 300 env GPUHASH_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 ;;
+        inproc) run inproc1 300 python -u bench.py --inproc 0 --steps 5 --warmup 1
+                run inproc2 300 python -u bench.py --inproc 0,0 --steps 3 --warmup 1 ;;
+        latency) run latency 120 python -u tools/latency.py ;;
         sweep) run sweep 600 python -u tools/layout_sweep.py ;;
         sys5) run sys5 900 python -u tools/system_bench.py ;;
         bench3) run bench3 300 python -u bench.py --config 3 --steps 5 --warmup 1 ;;
