@@ -165,31 +165,53 @@ inline uint32_t low_bytes_mask(int nbytes) {
     return (1u << (8 * nbytes)) - 1u;
 }
 
-void build_launch(const uint8_t* msg, uint64_t m, const GroupLayout& g, uint64_t H,
+// Chaining state after the leading blocks that hold message bytes only (they are the
+// same for every digit group and launch of a search, so plan_range compresses them once).
+struct Prefix {
+    uint64_t blocks = 0;  // floor(m / 64): block `blocks` is the first that holds ' '
+    uint32_t st[8];
+};
+
+Prefix make_prefix(const uint8_t* msg, uint64_t m) {
+    Prefix p;
+    std::memcpy(p.st, kIV, 32);
+    p.blocks = m / 64;
+    for (uint64_t b = 0; b < p.blocks; b++) {
+        uint32_t w[16];
+        for (int i = 0; i < 16; i++) w[i] = be32(msg + b * 64 + 4 * (uint64_t)i);
+        sha256_compress(p.st, w);
+    }
+    return p;
+}
+
+void build_launch(const uint8_t* msg, uint64_t m, const Prefix& pre, const GroupLayout& g, uint64_t H,
                   uint64_t lo, uint64_t hi, uint32_t rchunk_max, Launch& out) {
     const int d = g.d, q = g.q, s = g.s, h = d - s - q;
     const uint64_t L = m + 1 + (uint64_t)d;
     const uint64_t nblk = g.B + 1 + (uint64_t)g.EX;
-    std::vector<uint8_t> buf(nblk * 64, 0);
-    if (m) std::memcpy(buf.data(), msg, m);
-    buf[m] = ' ';
+    const uint64_t first_var = g.C2 ? g.B - 1 : g.B;
+    // pre.blocks <= first_var: the first digit is at byte m+1, and block B-1 of a C2
+    // layout holds digits, so it cannot lie wholly inside the message
+    const uint64_t p0 = pre.blocks, base = 64 * p0;
+    std::vector<uint8_t> buf((nblk - p0) * 64, 0);  // blocks p0 .. nblk-1
+    if (m > base) std::memcpy(buf.data(), msg + base, m - base);
+    buf[m - base] = ' ';
     // the h leading digits (H has exactly h digits; H == 0 when h == 0)
     uint64_t v = H;
-    for (int i = h - 1; i >= 0; i--) { buf[m + 1 + (uint64_t)i] = (uint8_t)('0' + v % 10u); v /= 10u; }
+    for (int i = h - 1; i >= 0; i--) { buf[m + 1 + (uint64_t)i - base] = (uint8_t)('0' + v % 10u); v /= 10u; }
     // lane + loop digit bytes stay 0: the kernel ORs ASCII into them
-    buf[L] = 0x80;
+    buf[L - base] = 0x80;
     uint64_t bits = L * 8u;
-    for (int i = 0; i < 8; i++) buf[nblk * 64 - 1 - (uint64_t)i] = (uint8_t)(bits >> (8 * i));
+    for (int i = 0; i < 8; i++) buf[(nblk - p0) * 64 - 1 - (uint64_t)i] = (uint8_t)(bits >> (8 * i));
     auto words = [&](uint64_t blk, uint32_t w[16]) {
-        for (int i = 0; i < 16; i++) w[i] = be32(&buf[blk * 64 + 4 * (uint64_t)i]);
+        for (int i = 0; i < 16; i++) w[i] = be32(&buf[(blk - p0) * 64 + 4 * (uint64_t)i]);
     };
 
     LaunchDesc& D = out.desc;
     std::memset(&D, 0, sizeof D);
     uint32_t st[8];
-    std::memcpy(st, kIV, 32);
-    const uint64_t first_var = g.C2 ? g.B - 1 : g.B;
-    for (uint64_t b = 0; b < first_var; b++) {
+    std::memcpy(st, pre.st, 32);
+    for (uint64_t b = p0; b < first_var; b++) {
         uint32_t w[16];
         words(b, w);
         sha256_compress(st, w);
@@ -252,6 +274,7 @@ void build_launch(const uint8_t* msg, uint64_t m, const GroupLayout& g, uint64_t
 void plan_range(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper,
                 std::vector<Launch>& out, uint32_t rchunk_max, int policy) {
     const int dlo = num_digits(lower), dhi = num_digits(upper);
+    const Prefix pre = make_prefix(msg, len);
     for (int d = dlo; d <= dhi; d++) {
         uint64_t a = d == 1 ? 0 : pow10u(d - 1);
         uint64_t b = d == 20 ? UINT64_MAX : pow10u(d) - 1;
@@ -265,7 +288,7 @@ void plan_range(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper
             uint64_t lo = std::max(a, H * U);
             uint64_t hi = (H == Hl) ? b : H * U + (U - 1);
             Launch l;
-            build_launch(msg, len, g, H, lo, hi, rchunk_max, l);
+            build_launch(msg, len, pre, g, H, lo, hi, rchunk_max, l);
             out.push_back(l);
             if (H == Hl) break;
         }
