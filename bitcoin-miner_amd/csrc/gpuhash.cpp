@@ -9,6 +9,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <thread>
@@ -55,6 +56,9 @@ struct Dev {
 }  // namespace
 
 struct gpuhash_ctx {
+    // One search at a time per context (a miner runs one job at a time, p1.pdf p.13);
+    // concurrent callers, e.g. several goroutines sharing an Engine, are serialised here.
+    std::mutex mu;
     std::vector<Dev> devs;
     int policy = kLayoutAuto;
     gpuhash_stats last{};
@@ -315,6 +319,7 @@ int gpuhash_ndevices(const gpuhash_ctx* ctx) { return ctx ? (int)ctx->devs.size(
 
 int gpuhash_set_layout_policy(gpuhash_ctx* ctx, int policy) {
     if (!ctx || policy < GPUHASH_LAYOUT_AUTO || policy > GPUHASH_LAYOUT_CLASSIC) return GPUHASH_EINVAL;
+    std::lock_guard<std::mutex> lock(ctx->mu);
     ctx->policy = policy;
     return GPUHASH_OK;
 }
@@ -364,6 +369,7 @@ int gpuhash_min_ex(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uint64_
     if (!ctx || !out_hash || !out_nonce || (msg_len && !msg)) return GPUHASH_EINVAL;
     if (lower > upper) return GPUHASH_EINVAL;
     if (msg_len > GPUHASH_MAX_MSG) return GPUHASH_ETOOLONG;
+    std::lock_guard<std::mutex> lock(ctx->mu);
     try {
         auto t0 = std::chrono::steady_clock::now();
         const uint64_t n = ctx->devs.size();
@@ -425,6 +431,7 @@ int gpuhash_hash_range(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uin
     if (count == 0) return GPUHASH_OK;
     if (count > (1ull << 26) || lower + (count - 1) < lower) return GPUHASH_EINVAL;
     if (msg_len > GPUHASH_MAX_MSG) return GPUHASH_ETOOLONG;
+    std::lock_guard<std::mutex> lock(ctx->mu);
     auto t0 = std::chrono::steady_clock::now();
     Dev& d = ctx->devs[0];
     for (auto& x : ctx->devs) x.used = false;
@@ -458,12 +465,14 @@ uint64_t gpuhash_hash_cpu(const uint8_t* msg, size_t msg_len, uint64_t nonce) {
 
 int gpuhash_last_stats(const gpuhash_ctx* ctx, gpuhash_stats* out) {
     if (!ctx || !out) return GPUHASH_EINVAL;
+    std::lock_guard<std::mutex> lock(const_cast<gpuhash_ctx*>(ctx)->mu);
     *out = ctx->last;
     return GPUHASH_OK;
 }
 
 int gpuhash_last_launches(const gpuhash_ctx* ctx, gpuhash_launch_record* out, int cap) {
     if (!ctx || cap < 0 || (cap > 0 && !out)) return GPUHASH_EINVAL;
+    std::lock_guard<std::mutex> lock(const_cast<gpuhash_ctx*>(ctx)->mu);
     const int n = (int)ctx->recs.size();
     for (int i = 0; i < n && i < cap; i++) out[i] = ctx->recs[(size_t)i];
     return n;

@@ -21,6 +21,10 @@
  *                  hash, and among equal hashes the lowest nonce (what an ascending
  *                  scan with strict '<' returns).  Overflow-safe at upper = 2^64-1.
  *
+ * Threading: calls on one context are serialised internally (a second caller waits);
+ * separate contexts run concurrently.  gpuhash_close must not race other calls on
+ * the same context.
+ *
  * Errors are negative return codes (gpuhash_strerror); nothing is printed.  The HIP
  * path is the only compute path: with no usable device gpuhash_open fails with
  * GPUHASH_ENODEV -- there is no silent CPU fallback.

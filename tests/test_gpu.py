@@ -269,3 +269,21 @@ def test_top_of_u64_range_in_slices(engine, monkeypatch):
     lo = U64 - 3 * (1 << 20) + 1
     h, n = engine.min(b"bradfitz", lo, U64)
     assert lo <= n <= U64 and gpuhash.Hash(b"bradfitz", n) == h
+
+
+def test_concurrent_calls_on_one_context_are_serialised(engine, oracle):
+    """Several host threads sharing one context (e.g. goroutines sharing a Go Engine)
+    each get their own correct answer."""
+    import threading
+    jobs = [(b"bradfitz", i * 50_000, i * 50_000 + 49_999) for i in range(8)]
+    got = [None] * len(jobs)
+
+    def run(i):
+        got[i] = engine.min(*jobs[i])
+
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(len(jobs))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    assert got == [oracle.min(*j) for j in jobs]
