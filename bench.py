@@ -120,6 +120,28 @@ def pmc_issued(key) -> float | None:
         return None
 
 
+_JSON_FD = None
+
+
+def _quiet_stdout() -> None:
+    """Keeps stdout for the ONE result line: fd 1 is pointed at stderr for the rest of the
+    run, so library banners (RCCL prints its version block to stdout at communicator
+    init) cannot land next to it; emit() writes to the saved original stdout."""
+    global _JSON_FD
+    sys.stdout.flush()
+    _JSON_FD = os.dup(1)
+    os.dup2(2, 1)
+
+
+def emit(out: dict) -> None:
+    line = (json.dumps(out) + "\n").encode()
+    if _JSON_FD is None:
+        sys.stdout.write(line.decode())
+        sys.stdout.flush()
+    else:
+        os.write(_JSON_FD, line)
+
+
 def main_inproc(args) -> None:
     """All devices in ONE process: each step is one gpuhash_min over the union of the
     per-GPU windows of ranks 0..N-1 (config 2/4: [0, N*per_gpu), weak scaling; config 3:
@@ -167,7 +189,7 @@ def main_inproc(args) -> None:
         "per_gpu_GHs": round(value / n, 4), "result": list(res),
         "launches_per_step": len(recs) // max(args.steps, 1),
     }
-    print(json.dumps(out), flush=True)
+    emit(out)
     eng.close()
 
 
@@ -185,6 +207,7 @@ def main() -> None:
                          "stream per device, 16-byte host argmin (SURVEY 8(e)); not used by "
                          "the torchrun path")
     args = ap.parse_args()
+    _quiet_stdout()
     if args.inproc is not None:
         return main_inproc(args)
 
@@ -198,7 +221,9 @@ def main() -> None:
     backend = os.environ.get("GPUHASH_DIST_BACKEND", "nccl")
     ndev = max(torch.cuda.device_count(), 1)
     local = local % ndev
-    if world > 1:
+    # GPUHASH_FORCE_DIST=1 runs the collective path even at WORLD_SIZE=1, so a 1-GPU box
+    # exercises the RCCL init / all_gather / all_reduce calls the 8-GPU run makes
+    if world > 1 or os.environ.get("GPUHASH_FORCE_DIST") == "1":
         import torch.distributed as dist
         torch.cuda.set_device(local)
         if backend == "nccl":
@@ -306,7 +331,7 @@ def main() -> None:
         if world == 1 and not args.no_cpu_baseline and args.config == "2":
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
             out["cpu_baseline_multicore"] = cpu_baseline_multicore(args.cpu_seconds / 2)
-        print(json.dumps(out), flush=True)
+        emit(out)
     eng.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -34,6 +34,7 @@ for step in "$@"; do
         systest) run pytest_sys 600 python -u -m pytest tests/test_gpu_system.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 300 python -u bench.py --steps 10 --warmup 2 ;;
+        nccl1) run nccl1 300 env GPUHASH_FORCE_DIST=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29541 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
         dist2) run dist2 300 env GPUHASH_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 ;;
         inproc) run inproc1 300 python -u bench.py --inproc 0 --steps 5 --warmup 1
                 run inproc2 300 python -u bench.py --inproc 0,0 --steps 3 --warmup 1 ;;
