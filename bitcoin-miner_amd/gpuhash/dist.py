@@ -62,22 +62,20 @@ def _pack(res: tuple[int, int] | None):
     return torch.from_numpy(arr.view(np.int64).copy())
 
 
-def _unpack(t) -> tuple[int, int] | None:
-    import numpy as np
-    a = t.cpu().numpy().view(np.uint64)
-    return (int(a[0]), int(a[1])) if int(a[2]) else None
-
-
 def gather_results(res: tuple[int, int] | None, device=None) -> list[tuple[int, int] | None]:
-    """all_gather of each rank's (hash, nonce) -- 24 bytes per rank."""
+    """all_gather of each rank's (hash, nonce) -- 24 bytes per rank, one collective into
+    one tensor and one copy back to the host."""
+    import numpy as np
     import torch
     import torch.distributed as dist
     t = _pack(res)
     if device is not None:
         t = t.to(device)
-    outs = [torch.empty_like(t) for _ in range(dist.get_world_size())]
-    dist.all_gather(outs, t)
-    return [_unpack(o) for o in outs]
+    world = dist.get_world_size()
+    out = torch.empty(3 * world, dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, t)
+    a = out.cpu().numpy().view(np.uint64).reshape(world, 3)
+    return [(int(h), int(n)) if int(v) else None for h, n, v in a]
 
 
 def distributed_min(search: Callable[[int, int], tuple[int, int]], lower: int, upper: int,
