@@ -1,8 +1,9 @@
-// kernels.hip -- instantiates the gfx950 scan kernels and the candidate reduce.
+// kernels.hip -- launch dispatch for the gfx950 scan kernels (instantiated in
+// kernels_{plain,ut,misc}.hip, see scan_decl.h) and the candidate reduce.
 #include <atomic>
 
 #include "kernels.h"
-#include "scan_kernel.h"
+#include "scan_decl.h"
 
 namespace gpuhash {
 
@@ -39,24 +40,6 @@ __global__ __launch_bounds__(1024) void k_reduce(Cand* __restrict__ cands,
         }
         *ncand = 0u;
     }
-}
-
-// Uniform schedule table of a C2/J=0 descriptor (one thread per loop value r):
-// tab[64*r + t] = K[t] + W_t, W = block B's uniform words with r's ASCII digits in W_0.
-__global__ __launch_bounds__(256) void k_ktab(const LaunchDesc* __restrict__ desc,
-                                              uint32_t* __restrict__ tab, uint32_t R) {
-    using namespace dev;
-    const uint32_t r = blockIdx.x * 256u + threadIdx.x;
-    if (r >= R) return;
-    const LaunchDesc& D = *desc;
-    uint32_t w[64];
-#pragma unroll
-    for (int i = 0; i < 16; i++) w[i] = D.U[i];
-    w[0] |= (ascii4(r) & D.qmask) << D.loop_shift;
-    expand_full(w);
-    uint32_t* out = tab + 64ull * r;
-#pragma unroll
-    for (int t = 0; t < 64; t++) out[t] = K[t] + w[t];
 }
 
 template <int J, int C2, bool EX, int MODE>

@@ -1,0 +1,17 @@
+// kernels_misc.hip -- k_scan instances built with the default code-generation options:
+// the classic straddling layout (C2 = 1, J = 1), the two-word uniform loop (C2 = 2) and
+// the extra-padding-block layouts (EX, J = 13..15), which measured no better (or worse,
+// EX at 8 waves/SIMD: -3%) under the plain/UT options (profiles/r01_variants.jsonl).
+#include "scan_decl.h"
+#include "scan_kernel.h"
+
+GPUHASH_INSTANTIATE_SCAN(1, 1, false, 0);
+GPUHASH_INSTANTIATE_SCAN(1, 1, false, 1);
+GPUHASH_INSTANTIATE_SCAN(1, 2, false, 0);
+GPUHASH_INSTANTIATE_SCAN(1, 2, false, 1);
+GPUHASH_INSTANTIATE_SCAN(13, 0, true, 0);
+GPUHASH_INSTANTIATE_SCAN(13, 0, true, 1);
+GPUHASH_INSTANTIATE_SCAN(14, 0, true, 0);
+GPUHASH_INSTANTIATE_SCAN(14, 0, true, 1);
+GPUHASH_INSTANTIATE_SCAN(15, 0, true, 0);
+GPUHASH_INSTANTIATE_SCAN(15, 0, true, 1);

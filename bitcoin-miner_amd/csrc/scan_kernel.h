@@ -364,8 +364,15 @@ __device__ __forceinline__ unsigned long long uniform64(unsigned long long v) {
 // amortise the per-row setup and the last ones are short, which keeps the tail of the
 // launch to ~gmin iterations.  The wave-uniform best (and its pruning word) persists
 // across pieces; each workgroup appends one 16-byte candidate at the end if it found one.
+// Tuning hook (tools/build_variants.sh): -DGPUHASH_WAVES_PER_EU=N asks for >= N waves per
+// SIMD, i.e. a VGPR budget of 512/N.  Off in the product build.
+#ifdef GPUHASH_WAVES_PER_EU
+#define GPUHASH_SCAN_ATTR __attribute__((amdgpu_waves_per_eu(GPUHASH_WAVES_PER_EU)))
+#else
+#define GPUHASH_SCAN_ATTR
+#endif
 template <int J, int C2, bool EX, int MODE>
-__global__ __launch_bounds__(256) void k_scan(const LaunchDesc* __restrict__ descs,
+__global__ __launch_bounds__(256) GPUHASH_SCAN_ATTR void k_scan(const LaunchDesc* __restrict__ descs,
                                               const unsigned long long* __restrict__ offs,
                                               int ndesc, unsigned long long* __restrict__ work,
                                               unsigned int gmin, unsigned int gmax,
