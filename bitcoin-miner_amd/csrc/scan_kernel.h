@@ -292,6 +292,12 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
         return;
     }
 
+    // tuning hook (tools/build_variants.sh): -DGPUHASH_R_UNROLL=N interleaves N nonces
+#ifdef GPUHASH_R_UNROLL
+#pragma unroll GPUHASH_R_UNROLL
+#else
+#pragma unroll 1
+#endif
     for (uint32_t r = r0; r < r1; r++) {
         uint32_t H0, H1;
         if constexpr (UT) {
