@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Randomised GPU-vs-oracle parity soak (run on the GPU box; not part of the test suite).
+
+Draws (message, range) cases across message lengths 0-300 (plus a few 1-4 KB), every
+digit count 1-20, ranges of 1 to ~2e6 nonces placed at random or straddling a digit-count
+boundary, under every layout policy, and compares gpuhash_min with the C oracle's scan.
+Prints one JSON line per 100 cases and a summary; exits 1 on the first mismatch.
+"""
+import json
+import os
+import random
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "bitcoin-miner_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import gpuhash  # noqa: E402
+import hash_oracle  # noqa: E402
+
+U64 = (1 << 64) - 1
+seconds = float(sys.argv[1]) if len(sys.argv) > 1 else 120.0
+seed = int(sys.argv[2]) if len(sys.argv) > 2 else 12345
+rng = random.Random(seed)
+oracle = hash_oracle.load_c_oracle()
+threads = min(16, len(os.sched_getaffinity(0)))
+
+
+def case():
+    mlen = rng.choice([rng.randrange(0, 301)] * 9 + [rng.randrange(1000, 4097)])
+    m = bytes(rng.randrange(256) for _ in range(mlen))
+    d = rng.randrange(1, 21)
+    lo_d = 0 if d == 1 else 10 ** (d - 1)
+    hi_d = U64 if d == 20 else 10 ** d - 1
+    n = int(10 ** rng.uniform(0, 6.3))
+    if rng.random() < 0.4 and d > 1:  # straddle the boundary into d digits
+        lo = max(0, lo_d - rng.randrange(0, n + 1))
+    else:
+        lo = rng.randrange(lo_d, hi_d + 1)
+    hi = min(U64, lo + n - 1)
+    return m, lo, hi
+
+
+t0 = time.time()
+count = nonces = 0
+with gpuhash.Engine([0]) as eng:
+    while time.time() - t0 < seconds:
+        m, lo, hi = case()
+        policy = rng.choice([gpuhash.LAYOUT_AUTO, gpuhash.LAYOUT_UNIFORM, gpuhash.LAYOUT_CLASSIC])
+        eng.set_layout_policy(policy)
+        got = eng.min(m, lo, hi)
+        want = oracle.min(m, lo, hi, threads=threads)
+        count += 1
+        nonces += hi - lo + 1
+        if got != want:
+            print(json.dumps({"MISMATCH": True, "msg_hex": m.hex(), "lower": lo, "upper": hi,
+                              "policy": policy, "got": list(got), "want": list(want)}), flush=True)
+            sys.exit(1)
+        if count % 100 == 0:
+            print(json.dumps({"cases": count, "nonces": nonces, "elapsed_s": round(time.time() - t0, 1)}),
+                  flush=True)
+print(json.dumps({"summary": True, "cases": count, "nonces": nonces, "mismatches": 0, "seed": seed,
+                  "elapsed_s": round(time.time() - t0, 1)}), flush=True)
