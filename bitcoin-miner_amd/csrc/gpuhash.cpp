@@ -29,6 +29,10 @@ constexpr uint64_t kSlicePerDevice = 1ull << 38;
 struct Dev {
     int ord = -1;
     hipStream_t stream = nullptr;
+    // side stream: the smaller kernel variants of a call run here, concurrently with the
+    // dominant one, so their launch and tail overlap its work instead of adding to it
+    hipStream_t side = nullptr;
+    hipEvent_t ev_ready = nullptr, ev_join = nullptr;
     unsigned long long* d_thresh = nullptr;
     Cand* d_cands = nullptr;
     unsigned int* d_ncand = nullptr;
@@ -74,6 +78,9 @@ static int dev_init(Dev& d, int ord) {
     d.ord = ord;
     HIPCHK(hipSetDevice(ord));
     HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&d.side, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&d.ev_ready, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&d.ev_join, hipEventDisableTiming));
     if (hipMalloc(&d.d_thresh, sizeof(unsigned long long)) != hipSuccess) return GPUHASH_ENOMEM;
     if (hipMalloc(&d.d_ncand, sizeof(unsigned int)) != hipSuccess) return GPUHASH_ENOMEM;
     if (hipMalloc(&d.d_best, sizeof(Cand)) != hipSuccess) return GPUHASH_ENOMEM;
@@ -86,6 +93,9 @@ static void dev_free(Dev& d) {
     if (d.ord < 0) return;
     hipSetDevice(d.ord);
     if (d.stream) hipStreamSynchronize(d.stream);
+    if (d.side) hipStreamSynchronize(d.side);
+    if (d.ev_ready) hipEventDestroy(d.ev_ready);
+    if (d.ev_join) hipEventDestroy(d.ev_join);
     for (auto e : d.ev) hipEventDestroy(e);
     d.ev.clear();
     if (d.d_thresh) hipFree(d.d_thresh);
@@ -97,6 +107,7 @@ static void dev_free(Dev& d) {
     if (d.d_ktab) hipFree(d.d_ktab);
     if (d.h_meta) hipHostFree(d.h_meta);
     if (d.stream) hipStreamDestroy(d.stream);
+    if (d.side) hipStreamDestroy(d.side);
     d = Dev{};
 }
 
@@ -185,7 +196,6 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
     int rc = dev_reserve_meta(d, bytes);
     if (rc) return rc;
     std::memset(d.h_meta, 0, 8 * groups.size());
-    uint32_t maxgrid = 1;
     std::vector<unsigned int> grids(groups.size());
     // C2/J=0 tables: block B's words depend only on the digit count d, so one table per
     // d serves every descriptor of that digit group; built by k_ktab from the device
@@ -219,9 +229,11 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
         // no more workgroups than minimum-size pieces
         unsigned long long pieces = (acc + 9) / 10;
         grids[g] = (unsigned int)std::min<unsigned long long>(full, std::max<unsigned long long>(pieces, 1));
-        maxgrid = std::max(maxgrid, grids[g]);
     }
-    rc = dev_reserve(d, maxgrid, 2 * groups.size());
+    // every workgroup of every group may append one candidate before the single reduce
+    uint32_t sumgrid = 0;
+    for (unsigned int gr : grids) sumgrid += gr;
+    rc = dev_reserve(d, std::max<uint32_t>(sumgrid, 1u), 2 * groups.size());
     if (rc) return rc;
     if (tab_words && (rc = dev_reserve_ktab(d, tab_words))) return rc;
     HIPCHK(hipMemcpyAsync(d.d_meta, d.h_meta, bytes, hipMemcpyHostToDevice, d.stream));
@@ -233,9 +245,30 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
     HIPCHK(hipMemsetAsync(d.d_ncand, 0, sizeof(unsigned int), d.stream));
     const unsigned int gmax = rchunk ? rchunk : 400u;
     const unsigned int gmin = std::min(10u, gmax);
+    // The group with the most row-iterations runs on the main stream; the others go
+    // first, on the side stream, so the dominant persistent grid fills whatever slots
+    // they leave and keeps its work-stealing running through their tails.  All groups
+    // append to one candidate list (atomic counter, shared pruning threshold); one
+    // reduce after the join folds it.
+    size_t big = 0;
+    unsigned long long big_work = 0;
     for (size_t g = 0; g < groups.size(); g++) {
+        const auto* offs = reinterpret_cast<const unsigned long long*>(d.h_meta + offs_at[g]);
+        const unsigned long long w = offs[groups[g].idx.size()];
+        if (g == 0 || w > big_work) { big = g; big_work = w; }
+    }
+    const bool use_side = groups.size() > 1;
+    if (use_side) {
+        HIPCHK(hipEventRecord(d.ev_ready, d.stream));
+        HIPCHK(hipStreamWaitEvent(d.side, d.ev_ready, 0));
+    }
+    std::vector<size_t> order;
+    for (size_t g = 0; g < groups.size(); g++)
+        if (g != big) order.push_back(g);
+    order.push_back(big);
+    for (size_t g : order) {
         ScanArgs a{};
-        a.stream = d.stream;
+        a.stream = (use_side && g != big) ? d.side : d.stream;
         a.descs = reinterpret_cast<const LaunchDesc*>(d.d_meta + desc_at[g]);
         a.offs = reinterpret_cast<const unsigned long long*>(d.d_meta + offs_at[g]);
         a.ndesc = (int)groups[g].idx.size();
@@ -249,11 +282,15 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
         a.dump_lo = lo;
         a.ktab = d.d_ktab;
         a.grid = grids[g];
-        HIPCHK(hipEventRecord(d.ev[2 * g], d.stream));
+        HIPCHK(hipEventRecord(d.ev[2 * g], a.stream));
         HIPCHK(launch_scan(groups[g].J, groups[g].C2, groups[g].EX, mode, a));
-        HIPCHK(hipEventRecord(d.ev[2 * g + 1], d.stream));
-        if (mode == 0) HIPCHK(launch_reduce(d.d_cands, d.d_ncand, d.d_best, d.stream));
+        HIPCHK(hipEventRecord(d.ev[2 * g + 1], a.stream));
     }
+    if (use_side) {
+        HIPCHK(hipEventRecord(d.ev_join, d.side));
+        HIPCHK(hipStreamWaitEvent(d.stream, d.ev_join, 0));
+    }
+    if (mode == 0) HIPCHK(launch_reduce(d.d_cands, d.d_ncand, d.d_best, d.stream));
     HIPCHK(hipMemcpyAsync(d.h_best, d.d_best, sizeof(Cand), hipMemcpyDeviceToHost, d.stream));
     HIPCHK(hipStreamSynchronize(d.stream));
     for (size_t g = 0; g < groups.size(); g++) {
