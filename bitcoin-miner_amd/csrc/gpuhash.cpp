@@ -29,10 +29,6 @@ constexpr uint64_t kSlicePerDevice = 1ull << 38;
 struct Dev {
     int ord = -1;
     hipStream_t stream = nullptr;
-    // side stream: the smaller kernel variants of a call run here, concurrently with the
-    // dominant one, so their launch and tail overlap its work instead of adding to it
-    hipStream_t side = nullptr;
-    hipEvent_t ev_ready = nullptr, ev_join = nullptr;
     unsigned long long* d_thresh = nullptr;
     Cand* d_cands = nullptr;
     unsigned int* d_ncand = nullptr;
@@ -78,9 +74,6 @@ static int dev_init(Dev& d, int ord) {
     d.ord = ord;
     HIPCHK(hipSetDevice(ord));
     HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&d.side, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&d.ev_ready, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&d.ev_join, hipEventDisableTiming));
     if (hipMalloc(&d.d_thresh, sizeof(unsigned long long)) != hipSuccess) return GPUHASH_ENOMEM;
     if (hipMalloc(&d.d_ncand, sizeof(unsigned int)) != hipSuccess) return GPUHASH_ENOMEM;
     if (hipMalloc(&d.d_best, sizeof(Cand)) != hipSuccess) return GPUHASH_ENOMEM;
@@ -93,9 +86,6 @@ static void dev_free(Dev& d) {
     if (d.ord < 0) return;
     hipSetDevice(d.ord);
     if (d.stream) hipStreamSynchronize(d.stream);
-    if (d.side) hipStreamSynchronize(d.side);
-    if (d.ev_ready) hipEventDestroy(d.ev_ready);
-    if (d.ev_join) hipEventDestroy(d.ev_join);
     for (auto e : d.ev) hipEventDestroy(e);
     d.ev.clear();
     if (d.d_thresh) hipFree(d.d_thresh);
@@ -107,7 +97,6 @@ static void dev_free(Dev& d) {
     if (d.d_ktab) hipFree(d.d_ktab);
     if (d.h_meta) hipHostFree(d.h_meta);
     if (d.stream) hipStreamDestroy(d.stream);
-    if (d.side) hipStreamDestroy(d.side);
     d = Dev{};
 }
 
@@ -245,30 +234,15 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
     HIPCHK(hipMemsetAsync(d.d_ncand, 0, sizeof(unsigned int), d.stream));
     const unsigned int gmax = rchunk ? rchunk : 400u;
     const unsigned int gmin = std::min(10u, gmax);
-    // The group with the most row-iterations runs on the main stream; the others go
-    // first, on the side stream, so the dominant persistent grid fills whatever slots
-    // they leave and keeps its work-stealing running through their tails.  All groups
-    // append to one candidate list (atomic counter, shared pruning threshold); one
-    // reduce after the join folds it.
-    size_t big = 0;
-    unsigned long long big_work = 0;
+    // Groups run back to back on the device's stream (each launch's HIP events then time
+    // that kernel alone, which bench.py's roofline relies on).  Running the small groups
+    // on a second stream was measured: a persistent grid launched beside another is not
+    // fully dispatched until the other drains, so its events span the whole call, for
+    // <= 0.3% less wall time.  All groups append to one candidate list (atomic counter,
+    // shared pruning threshold); one reduce at the end folds it.
     for (size_t g = 0; g < groups.size(); g++) {
-        const auto* offs = reinterpret_cast<const unsigned long long*>(d.h_meta + offs_at[g]);
-        const unsigned long long w = offs[groups[g].idx.size()];
-        if (g == 0 || w > big_work) { big = g; big_work = w; }
-    }
-    const bool use_side = groups.size() > 1;
-    if (use_side) {
-        HIPCHK(hipEventRecord(d.ev_ready, d.stream));
-        HIPCHK(hipStreamWaitEvent(d.side, d.ev_ready, 0));
-    }
-    std::vector<size_t> order;
-    for (size_t g = 0; g < groups.size(); g++)
-        if (g != big) order.push_back(g);
-    order.push_back(big);
-    for (size_t g : order) {
         ScanArgs a{};
-        a.stream = (use_side && g != big) ? d.side : d.stream;
+        a.stream = d.stream;
         a.descs = reinterpret_cast<const LaunchDesc*>(d.d_meta + desc_at[g]);
         a.offs = reinterpret_cast<const unsigned long long*>(d.d_meta + offs_at[g]);
         a.ndesc = (int)groups[g].idx.size();
@@ -285,10 +259,6 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
         HIPCHK(hipEventRecord(d.ev[2 * g], a.stream));
         HIPCHK(launch_scan(groups[g].J, groups[g].C2, groups[g].EX, mode, a));
         HIPCHK(hipEventRecord(d.ev[2 * g + 1], a.stream));
-    }
-    if (use_side) {
-        HIPCHK(hipEventRecord(d.ev_join, d.side));
-        HIPCHK(hipStreamWaitEvent(d.stream, d.ev_join, 0));
     }
     if (mode == 0) HIPCHK(launch_reduce(d.d_cands, d.d_ncand, d.d_best, d.stream));
     HIPCHK(hipMemcpyAsync(d.h_best, d.d_best, sizeof(Cand), hipMemcpyDeviceToHost, d.stream));

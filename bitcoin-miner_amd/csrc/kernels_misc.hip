@@ -1,7 +1,7 @@
-// kernels_misc.hip -- k_scan instances built with the default code-generation options:
-// the classic straddling layout (C2 = 1, J = 1), the two-word uniform loop (C2 = 2) and
-// the extra-padding-block layouts (EX, J = 13..15), which measured no better (or worse,
-// EX at 8 waves/SIMD: -3%) under the plain/UT options (profiles/r01_variants.jsonl).
+// kernels_misc.hip -- k_scan instances of the classic straddling layout (C2 = 1, J = 1),
+// the two-word uniform loop (C2 = 2) and the extra-padding-block layouts (EX, J = 13..15).
+// Built with -mllvm -amdgpu-sched-strategy=max-ilp (Makefile): classic +2.6%, EX +0.7%,
+// C2 = 2 -0.2% vs defaults; 8 waves/SIMD costs EX 3% (profiles/r01_variants.jsonl).
 #include "scan_decl.h"
 #include "scan_kernel.h"
 

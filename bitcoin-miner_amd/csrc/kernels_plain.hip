@@ -1,7 +1,7 @@
 // kernels_plain.hip -- k_scan instances of the plain layouts (C2 = 0, no extra block):
 // loop word W_J of the only nonce-bearing block, J = 0..13.  Built with
-// -DGPUHASH_WAVES_PER_EU=8 -mllvm -amdgpu-sched-strategy=max-ilp (Makefile): +1.1% on
-// config 2 over the default options (profiles/r01_variants.jsonl).
+// -DGPUHASH_WAVES_PER_EU=8 (Makefile): 8 waves/SIMD in 63 VGPRs without spills, +0.3% on
+// config 2 and +4% on J = 2 over the unconstrained build (profiles/r01_variants.jsonl).
 #include "scan_decl.h"
 #include "scan_kernel.h"
 

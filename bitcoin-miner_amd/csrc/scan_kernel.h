@@ -309,8 +309,10 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
 #pragma unroll
             for (int i = 0; i < 16; i++) w[i] = W[i];
             w[J] = WJ;
-            // schedule: loop-invariant terms summed first so LICM hoists them
-            sfor<16, 64>([&](auto tc) {
+            // schedule word t, computed just before round t uses it (so only the ~16
+            // words of the sliding window are live, not all 48): loop-invariant terms
+            // are summed first so LICM hoists them out of the r-loop
+            auto sched = [&](auto tc) {
                 constexpr int t = decltype(tc)::value;
                 constexpr bool d2 = kDep.v[t - 2], d7 = kDep.v[t - 7], d15 = kDep.v[t - 15], d16 = kDep.v[t - 16];
                 uint32_t x2, x15;
@@ -319,7 +321,7 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
                 uint32_t inv = (d2 ? 0u : x2) + (d7 ? 0u : w[t - 7]) + (d15 ? 0u : x15) + (d16 ? 0u : w[t - 16]);
                 uint32_t var = (d2 ? x2 : 0u) + (d7 ? w[t - 7] : 0u) + (d15 ? x15 : 0u) + (d16 ? w[t - 16] : 0u);
                 w[t] = inv + var;
-            });
+            };
             State x = s;
             {   // round J: everything but W_J is loop-invariant
                 uint32_t inv = x.h + bS1(x.e) + ch(x.e, x.f, x.g) + K[J];
@@ -329,9 +331,14 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
             }
             sfor<J + 1, 63>([&](auto tc) {
                 constexpr int t = decltype(tc)::value;
-                if constexpr (t < 16) round_kw(x, K[t] + w[t]);   // uniform word: K+W folds
-                else round_kw(x, w[t] + K[t]);
+                if constexpr (t < 16) {
+                    round_kw(x, K[t] + w[t]);   // uniform word: K+W folds
+                } else {
+                    sched(tc);
+                    round_kw(x, w[t] + K[t]);
+                }
             });
+            sched(std::integral_constant<int, 63>{});
             if constexpr (!EX) {
                 // round 63: e is dead; fold CV0 into the constant so a64 + CV0 is free
                 uint32_t t1 = x.h + w[63] + (K[63] + cv[0]) + ch(x.e, x.f, x.g) + bS1(x.e);

@@ -22,10 +22,7 @@ build() {  # build <name> <extra flags...>
 # the product build (per-family options from the Makefile) next to uniform-option builds
 mkdir -p tools/variants/product && cp bitcoin-miner_amd/lib/libgpuhash.so tools/variants/product/
 build base &
+build occ8 -DGPUHASH_WAVES_PER_EU=8 &
+build maxilp -mllvm -amdgpu-sched-strategy=max-ilp &
 build occ8_maxilp -DGPUHASH_WAVES_PER_EU=8 -mllvm -amdgpu-sched-strategy=max-ilp &
-build unroll2 -DGPUHASH_R_UNROLL=2 &
-build unroll2_maxilp -DGPUHASH_R_UNROLL=2 -mllvm -amdgpu-sched-strategy=max-ilp &
-wait
-build occ4_unroll2 -DGPUHASH_WAVES_PER_EU=4 -DGPUHASH_R_UNROLL=2 -mllvm -amdgpu-sched-strategy=max-ilp &
-build occ8_bias -DGPUHASH_WAVES_PER_EU=8 -mllvm -amdgpu-sched-strategy=max-ilp -mllvm -amdgpu-schedule-metric-bias=100 &
 wait
