@@ -274,8 +274,9 @@ def main() -> None:
     by = {}
     for r in recs:
         k = (r["J"], r["C2"], r["EX"])
-        e = by.setdefault(k, {"ms": 0.0, "n": 0, "nonces": 0, "c": r["c"]})
+        e = by.setdefault(k, {"ms": 0.0, "n": 0, "nonces": 0, "c": r["c"], "clk_ms": 0.0})
         e["ms"] += r["ms"]
+        e["clk_ms"] += r["sclk_mhz"] * r["ms"]  # ms-weighted in-kernel shader clock
         e["n"] += 1
         e["nonces"] += r["nonces"]
     key, dom = max(by.items(), key=lambda kv: kv[1]["ms"])
@@ -283,6 +284,8 @@ def main() -> None:
     ops_per_launch = dom["nonces"] / dom["n"] * OPS_PER_BLOCK * dom["c"]
     achieved_T = ops_per_launch / (avg_ms * 1e-3) / 1e12
     kernel_ghs = dom["nonces"] / (dom["ms"] * 1e-3) / 1e9
+    sclk = dom["clk_ms"] / dom["ms"] if dom["ms"] > 0 else 0.0  # MHz, measured in the kernel
+    peak_at_clk = 256 * 64 * sclk * 1e6 / 1e12  # T lane-ops/s at the measured clock
     insts = pmc_issued(key) if args.config == "2" else None  # PMC pass was config 2
     issued_per_nonce = insts * 64 / (dom["nonces"] / dom["n"]) if insts else None
 
@@ -326,6 +329,11 @@ def main() -> None:
                 # the guide's SIMD-32 nominal (2-cycle wave64 issue) rate: reachable only by
                 # streams without v_alignbit/v_add3, so not the bound here
                 "simd32_nominal_peak": round(VALU_PEAK_T * 2, 3),
+                # shader clock over the dominant launches, from s_memtime / s_memrealtime
+                # in workgroup 0 (record the sustained sclk beside every GH/s)
+                "sclk_mhz": round(sclk, 1),
+                "peak_at_sclk": round(peak_at_clk, 3),
+                "frac_at_sclk": round(achieved_T / peak_at_clk, 4) if peak_at_clk else None,
             },
         }
         if world == 1 and not args.no_cpu_baseline and args.config == "2":

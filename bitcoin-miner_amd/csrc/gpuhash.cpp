@@ -26,6 +26,10 @@ namespace {
 // one MI355X at config-2 rates.
 constexpr uint64_t kSlicePerDevice = 1ull << 38;
 
+// Per kernel-variant group in the launch metadata: the work counter, then the 4 clock words
+// the scan kernel writes (start/end s_memtime and s_memrealtime of workgroup 0).
+constexpr size_t kCounterBytes = 40;
+
 struct Dev {
     int ord = -1;
     hipStream_t stream = nullptr;
@@ -43,6 +47,9 @@ struct Dev {
     // uniform K+W tables of C2/J=0 descriptors (one per digit count), grow-only
     uint32_t* d_ktab = nullptr;
     size_t ktab_cap = 0;  // words
+    // pinned copy of the per-group work counters + clock samples (kCounterBytes each)
+    unsigned long long* h_clk = nullptr;
+    size_t clk_cap = 0;  // groups
     std::vector<hipEvent_t> ev;
     // per-call results
     int rc = GPUHASH_OK;
@@ -95,6 +102,7 @@ static void dev_free(Dev& d) {
     if (d.h_best) hipHostFree(d.h_best);
     if (d.d_meta) hipFree(d.d_meta);
     if (d.d_ktab) hipFree(d.d_ktab);
+    if (d.h_clk) hipHostFree(d.h_clk);
     if (d.h_meta) hipHostFree(d.h_meta);
     if (d.stream) hipStreamDestroy(d.stream);
     d = Dev{};
@@ -121,6 +129,17 @@ static int dev_reserve_ktab(Dev& d, size_t words) {
     d.ktab_cap = 0;
     if (hipMalloc(&d.d_ktab, words * sizeof(uint32_t)) != hipSuccess) return GPUHASH_ENOMEM;
     d.ktab_cap = words;
+    return GPUHASH_OK;
+}
+
+static int dev_reserve_clk(Dev& d, size_t groups) {
+    if (groups <= d.clk_cap) return GPUHASH_OK;
+    if (d.h_clk) hipHostFree(d.h_clk);
+    d.h_clk = nullptr;
+    d.clk_cap = 0;
+    const size_t n = std::max<size_t>(groups, 8);
+    if (hipHostMalloc(&d.h_clk, kCounterBytes * n, hipHostMallocDefault) != hipSuccess) return GPUHASH_ENOMEM;
+    d.clk_cap = n;
     return GPUHASH_OK;
 }
 
@@ -171,8 +190,9 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
         it->idx.push_back(i);
     }
 
-    // meta layout: [work counters: 8 B x groups][per group: offs (n+1) x 8 B, descs]
-    size_t bytes = 8 * groups.size();
+    // meta layout: [per group: work counter + 4 clock words, 40 B][per group: offs
+    // (n+1) x 8 B, descs]
+    size_t bytes = kCounterBytes * groups.size();
     std::vector<size_t> offs_at(groups.size()), desc_at(groups.size());
     for (size_t g = 0; g < groups.size(); g++) {
         offs_at[g] = bytes;
@@ -184,7 +204,7 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
     }
     int rc = dev_reserve_meta(d, bytes);
     if (rc) return rc;
-    std::memset(d.h_meta, 0, 8 * groups.size());
+    std::memset(d.h_meta, 0, kCounterBytes * groups.size());
     std::vector<unsigned int> grids(groups.size());
     // C2/J=0 tables: block B's words depend only on the digit count d, so one table per
     // d serves every descriptor of that digit group; built by k_ktab from the device
@@ -225,6 +245,7 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
     rc = dev_reserve(d, std::max<uint32_t>(sumgrid, 1u), 2 * groups.size());
     if (rc) return rc;
     if (tab_words && (rc = dev_reserve_ktab(d, tab_words))) return rc;
+    if ((rc = dev_reserve_clk(d, groups.size()))) return rc;
     HIPCHK(hipMemcpyAsync(d.d_meta, d.h_meta, bytes, hipMemcpyHostToDevice, d.stream));
     for (const Tab& t : tabs)
         HIPCHK(launch_ktab(reinterpret_cast<const LaunchDesc*>(d.d_meta + t.desc_byte), d.d_ktab + t.off,
@@ -246,7 +267,7 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
         a.descs = reinterpret_cast<const LaunchDesc*>(d.d_meta + desc_at[g]);
         a.offs = reinterpret_cast<const unsigned long long*>(d.d_meta + offs_at[g]);
         a.ndesc = (int)groups[g].idx.size();
-        a.work = reinterpret_cast<unsigned long long*>(d.d_meta + 8 * g);
+        a.work = reinterpret_cast<unsigned long long*>(d.d_meta + kCounterBytes * g);
         a.gmin = gmin;
         a.gmax = gmax;
         a.thresh = d.d_thresh;
@@ -262,6 +283,7 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
     }
     if (mode == 0) HIPCHK(launch_reduce(d.d_cands, d.d_ncand, d.d_best, d.stream));
     HIPCHK(hipMemcpyAsync(d.h_best, d.d_best, sizeof(Cand), hipMemcpyDeviceToHost, d.stream));
+    HIPCHK(hipMemcpyAsync(d.h_clk, d.d_meta, kCounterBytes * groups.size(), hipMemcpyDeviceToHost, d.stream));
     HIPCHK(hipStreamSynchronize(d.stream));
     for (size_t g = 0; g < groups.size(); g++) {
         float ms = 0;
@@ -275,8 +297,11 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
             nonces += n;
             if (!big || n > biggest) { big = &l; biggest = n; }
         }
+        const unsigned long long* c = d.h_clk + (kCounterBytes / 8) * g + 1;
+        const double ticks = (double)(c[2] - c[0]), rt = (double)(c[3] - c[1]);
+        const double sclk = rt > 0 ? ticks / rt * 100.0 : 0.0;  // s_memrealtime runs at 100 MHz
         d.recs.push_back(gpuhash_launch_record{d.ord, groups[g].J, groups[g].C2, groups[g].EX,
-                                               big->d, big->c, nonces, (double)ms});
+                                               big->d, big->c, nonces, (double)ms, sclk});
     }
     d.launches = (uint32_t)groups.size();
     d.best_h = d.h_best->hash;

@@ -17,7 +17,9 @@ struct ScanArgs {
     const LaunchDesc* descs;         // device: the group's launch descriptors
     const unsigned long long* offs;  // device: ndesc+1 prefix offsets in row-iterations
     int ndesc;
-    unsigned long long* work;        // device: guided-scheduling counter (zeroed per launch)
+    unsigned long long* work;        // device: guided-scheduling counter (zeroed per launch),
+                                     // followed by 4 clock words the kernel fills: s_memtime /
+                                     // s_memrealtime of workgroup 0 at its start and its end
     unsigned int gmin, gmax;         // piece size bounds (r values per grab)
     unsigned long long* thresh;      // pruning threshold (monotone atomicMin), per job
     Cand* cands;                     // appended per-workgroup candidates

@@ -30,6 +30,25 @@
 #include "kernels.h"
 #include "plan.h"
 
+// Code phase of the per-nonce loop bodies.  The same instruction stream runs ~3.5% faster
+// when the loop body starts at 4 mod 8 bytes than at 0 mod 8 (measured on config 2, J = 2,
+// J = 13 and config 3, profiles/r01_loop_phase.jsonl; the mechanism is in the instruction
+// fetch of the mixed 4-/8-byte encodings).  Without this, any edit before the loop flips
+// the phase at random.  ".p2align 3" + one s_nop pins it at 4 mod 8 for one or two s_nop
+// per iteration (~0.1%).  -DGPUHASH_LOOP_PHASE=0 / -1 selects phase 0 / no pinning; the
+// kernels_misc.hip layouts (classic straddle, extra block), insensitive to the phase,
+// build with -1.
+#ifndef GPUHASH_LOOP_PHASE
+#define GPUHASH_LOOP_PHASE 4
+#endif
+#if GPUHASH_LOOP_PHASE == 4
+#define GPUHASH_LOOP_ALIGN() asm volatile(".p2align 3\n\ts_nop 0")
+#elif GPUHASH_LOOP_PHASE == 0
+#define GPUHASH_LOOP_ALIGN() asm volatile(".p2align 3")
+#else
+#define GPUHASH_LOOP_ALIGN() ((void)0)
+#endif
+
 namespace gpuhash {
 
 namespace dev {
@@ -299,6 +318,7 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
 #pragma unroll 1
 #endif
     for (uint32_t r = r0; r < r1; r++) {
+        GPUHASH_LOOP_ALIGN();
         uint32_t H0, H1;
         if constexpr (UT) {
             const uint32_t* __restrict__ kw = ktab + D.tab_off + 64u * r;
@@ -404,6 +424,18 @@ __global__ __launch_bounds__(256) GPUHASH_SCAN_ATTR void k_scan(const LaunchDesc
     const uint32_t tid = threadIdx.x;
     const unsigned long long total = offs[ndesc];
 
+    // clock evidence: workgroup 0 (resident for the whole persistent launch) samples the
+    // shader clock counter and the 100 MHz real-time counter at its start and its end,
+    // into the 4 words after the group's work counter (no extra kernel argument: one
+    // measurably changed the hot loop's SGPR assignment and cost 3.5%)
+    unsigned long long* const clk = work + 1;
+#ifdef GPUHASH_PAD_NOPS  // experiment: shift the code that follows by 4 bytes per s_nop
+    asm volatile(".rept " GPUHASH_PAD_NOPS "\n\ts_nop 0\n\t.endr");
+#endif
+    if (blockIdx.x == 0 && tid == 0) {
+        clk[0] = __builtin_amdgcn_s_memtime();
+        clk[1] = __builtin_amdgcn_s_memrealtime();
+    }
     WaveBest wb{~0ull, ~0ull, 0xFFFFFFFFu};
     for (;;) {
         if (tid == 0) {
@@ -438,6 +470,10 @@ __global__ __launch_bounds__(256) GPUHASH_SCAN_ATTR void k_scan(const LaunchDesc
         }
     }
 
+    if (blockIdx.x == 0 && tid == 0) {
+        clk[2] = __builtin_amdgcn_s_memtime();
+        clk[3] = __builtin_amdgcn_s_memrealtime();
+    }
     if constexpr (MODE == 0) {
         const uint32_t wave = tid >> 6;
         if ((tid & 63u) == 0) { sh_best[wave][0] = wb.h; sh_best[wave][1] = wb.n; }

@@ -68,7 +68,7 @@ class Stats(ctypes.Structure):
 
 class LaunchRecord(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in ("device", "J", "C2", "EX", "digits", "c")] + [
-        ("nonces", ctypes.c_uint64), ("ms", ctypes.c_double)]
+        ("nonces", ctypes.c_uint64), ("ms", ctypes.c_double), ("sclk_mhz", ctypes.c_double)]
 
     def as_dict(self) -> dict:
         return {f: getattr(self, f) for f, _ in self._fields_}

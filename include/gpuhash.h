@@ -74,6 +74,8 @@ typedef struct gpuhash_launch_record {
     int32_t c;        /* 64-byte blocks holding nonce digits (1 or 2)               */
     uint64_t nonces;  /* nonces covered by the launch                               */
     double ms;        /* HIP-event time of the launch on the device's stream        */
+    double sclk_mhz;  /* shader clock over the launch, measured in the kernel:      */
+                      /*    s_memtime ticks / s_memrealtime (100 MHz) of workgroup 0 */
 } gpuhash_launch_record;
 
 /* Opens the listed devices (HIP ordinals); ndevices == 0 means every visible device.
