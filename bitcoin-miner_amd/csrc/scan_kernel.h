@@ -311,12 +311,7 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
         return;
     }
 
-    // tuning hook (tools/build_variants.sh): -DGPUHASH_R_UNROLL=N interleaves N nonces
-#ifdef GPUHASH_R_UNROLL
-#pragma unroll GPUHASH_R_UNROLL
-#else
-#pragma unroll 1
-#endif
+#pragma unroll 1  // one nonce per iteration (unrolling x2 measured no gain, r01_variants)
     for (uint32_t r = r0; r < r1; r++) {
         GPUHASH_LOOP_ALIGN();
         uint32_t H0, H1;
@@ -429,9 +424,6 @@ __global__ __launch_bounds__(256) GPUHASH_SCAN_ATTR void k_scan(const LaunchDesc
     // into the 4 words after the group's work counter (no extra kernel argument: one
     // measurably changed the hot loop's SGPR assignment and cost 3.5%)
     unsigned long long* const clk = work + 1;
-#ifdef GPUHASH_PAD_NOPS  // experiment: shift the code that follows by 4 bytes per s_nop
-    asm volatile(".rept " GPUHASH_PAD_NOPS "\n\ts_nop 0\n\t.endr");
-#endif
     if (blockIdx.x == 0 && tid == 0) {
         clk[0] = __builtin_amdgcn_s_memtime();
         clk[1] = __builtin_amdgcn_s_memrealtime();
