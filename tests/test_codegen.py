@@ -23,7 +23,8 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 def kernel_metadata(obj, tmp_path):
     fat = tmp_path / "fatbin.bin"
     co = tmp_path / "k.co"
-    subprocess.check_call(["objcopy", f"--dump-section=.hip_fatbin={fat}", obj])
+    # an explicit output file: objcopy with only an input rewrites it in place
+    subprocess.check_call(["objcopy", f"--dump-section=.hip_fatbin={fat}", obj, str(tmp_path / "copy.o")])
     subprocess.check_call([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o",
                            f"--input={fat}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"])
     notes = subprocess.check_output([os.path.join(LLVM, "llvm-readelf"), "--notes", str(co)], text=True)
@@ -103,7 +104,7 @@ def test_hot_loops_start_at_4_mod_8(tmp_path):
         d = tmp_path / tu
         d.mkdir(exist_ok=True)
         fat, co = d / "fatbin.bin", d / "k.co"
-        subprocess.check_call(["objcopy", f"--dump-section=.hip_fatbin={fat}", obj])
+        subprocess.check_call(["objcopy", f"--dump-section=.hip_fatbin={fat}", obj, str(d / "copy.o")])
         subprocess.check_call([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o",
                                f"--input={fat}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"])
         pins = [p for p in pinned_runs(co, kernel) if p is not None]
