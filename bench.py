@@ -309,6 +309,7 @@ def main() -> None:
                        "parallelism": f"dp{world}"},
             "per_gpu_GHs": round(value / world, 4),
             "result_rank0_range": list(res) if world == 1 else None,
+            "result": list(res),  # (hash, nonce) argmin over every rank's windows
             "roofline": {
                 "bound": "valu",
                 "achieved": round(achieved_T, 3),

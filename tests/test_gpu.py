@@ -178,6 +178,20 @@ def test_split_merge_invariance_at_scale(engine, oracle):
     assert lo <= whole[1] <= hi
 
 
+def test_config4_full_range(engine, oracle):
+    # Config 4 at full size: [0, 2^40) of "bradfitz" (~33 s on one MI355X).  The expected
+    # pair is GPU-derived, not an oracle golden (the C oracle would need ~60 h): three
+    # decompositions agreed on it -- one call, 8 cost-balanced in-process shards, and
+    # the 8 per-rank 2^37 windows of bench.py --config 4 merged on the host and through
+    # an 8-rank gloo run (profiles/r01_config4_full.jsonl).  Here it is re-derived and
+    # re-pinned by the oracle: the winner re-hashes, and an oracle scan of the 2^22
+    # nonces around it finds nothing lower (lowest nonce on ties).
+    h, n = engine.min(b"bradfitz", 0, (1 << 40) - 1)
+    assert (h, n) == (16555811, 890536971553)
+    assert oracle.hash(b"bradfitz", n) == h
+    assert oracle.min(b"bradfitz", n - (1 << 21), n + (1 << 21), threads=8) == (h, n)
+
+
 def test_errors_are_loud(engine):
     import gpuhash
     with pytest.raises(gpuhash.GpuHashError) as e:
