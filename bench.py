@@ -94,30 +94,37 @@ def cpu_baseline_multicore(seconds: float = 5.0) -> dict:
             "sample": f"oracle_min_mt over bradfitz [{lo}, {PER_GPU - 1}] ({n} nonces), {dt:.1f} s"}
 
 
-def pmc_traffic(key) -> float | None:
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC
-    summary (profiles/pmc_traffic.json: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE,
-    collected in separate --pmc passes by tools/gpu_session.sh pmc)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+# committed rocprofv3 PMC summary per bench config (tools/summarize_prof.py): each was
+# collected on the same bench.py workload, so its per-launch counters match this run's
+# launches of the same kernel
+PMC_SUMMARY = {"2": "r01_pmc_summary.json", "3": "r01c3_pmc_summary.json"}
+
+
+def _pmc_kernel(config: str, key) -> dict | None:
+    name = PMC_SUMMARY.get(config)
+    if name is None:
+        return None
     try:
-        with open(path) as f:
+        with open(os.path.join(ROOT, "profiles", name)) as f:
             t = json.load(f)
-        return t["kernels"][f"k_scan<{key[0]}, {int(key[1])}, {str(bool(key[2])).lower()}, 0>"]["hbm_bytes_per_launch"]
+        return t["kernels"][f"k_scan<{key[0]}, {int(key[1])}, {str(bool(key[2])).lower()}, 0>"]
     except (OSError, KeyError, ValueError):
         return None
 
 
-def pmc_issued(key) -> float | None:
-    """VALU wave-instructions per launch of the dominant kernel from the committed PMC
-    summary (SQ_INSTS_VALU, its own --pmc pass); x64 lanes / nonces = issued
-    lane-instructions per nonce, the hardware-counted work behind `achieved`."""
-    path = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
-    try:
-        with open(path) as f:
-            t = json.load(f)
-        return t["kernels"][f"k_scan<{key[0]}, {int(key[1])}, {str(bool(key[2])).lower()}, 0>"]["per_launch"]["SQ_INSTS_VALU"]
-    except (OSError, KeyError, ValueError):
-        return None
+def pmc_traffic(config: str, key) -> float | None:
+    """HBM bytes per launch of the dominant kernel: FETCH_SIZE x2 (gfx950 correction) +
+    WRITE_SIZE, collected in separate --pmc passes (tools/gpu_session.sh pmc / pmc3)."""
+    e = _pmc_kernel(config, key)
+    return e.get("hbm_bytes_per_launch") if e else None
+
+
+def pmc_issued(config: str, key) -> float | None:
+    """VALU wave-instructions per launch of the dominant kernel (SQ_INSTS_VALU, its own
+    --pmc pass); x64 lanes / nonces = issued lane-instructions per nonce, the
+    hardware-counted work behind `achieved`."""
+    e = _pmc_kernel(config, key)
+    return e["per_launch"].get("SQ_INSTS_VALU") if e else None
 
 
 _JSON_FD = None
@@ -286,7 +293,7 @@ def main() -> None:
     kernel_ghs = dom["nonces"] / (dom["ms"] * 1e-3) / 1e9
     sclk = dom["clk_ms"] / dom["ms"] if dom["ms"] > 0 else 0.0  # MHz, measured in the kernel
     peak_at_clk = 256 * 64 * sclk * 1e6 / 1e12  # T lane-ops/s at the measured clock
-    insts = pmc_issued(key) if args.config == "2" else None  # PMC pass was config 2
+    insts = pmc_issued(args.config, key)
     issued_per_nonce = insts * 64 / (dom["nonces"] / dom["n"]) if insts else None
 
     if rank == 0:
@@ -316,7 +323,7 @@ def main() -> None:
                 "peak": round(VALU_PEAK_T, 3),
                 "unit": "T int32 lane-ops/s",
                 "frac": round(achieved_T / VALU_PEAK_T, 4),
-                "traffic": pmc_traffic(key),
+                "traffic": pmc_traffic(args.config, key),
                 "kernel": f"k_scan<J={key[0]},C2={key[1]},EX={key[2]},MODE=0>",
                 "avg_launch_ms": round(avg_ms, 4),
                 "nonces_per_launch": dom["nonces"] / dom["n"],

@@ -2,7 +2,7 @@
 # tools/gpu_session.sh STEP... -- runs GPU steps on the gpurun box, each under its own
 # time limit, logging to gpurun_out/.  A plain failure (exit 1, e.g. a failing test)
 # lets the next step run; a fault, abort, segfault, time limit or kill stops the session.
-# Steps: valu | go | test | smoke | bench | bench3 | bench4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | sweep | sys5
+# Steps: valu | go | test | smoke | bench | bench3 | bench4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | pmc3 | sweep | sys5
 set -u
 cd "$(dirname "$0")/.."
 OUT=gpurun_out
@@ -50,6 +50,12 @@ for step in "$@"; do
              run pmc_derived 120 rocprofv3 --pmc VALUBusy VALUUtilization -d "$OUT/pmc4" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
              run pmc_hbm 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc2" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
              run pmc_wr 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc3" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+        pmc3) B3="python3 bench.py --config 3 --steps 2 --warmup 1 --no-cpu-baseline"
+              run prof_c3 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c3" -o bench --output-format csv -- $B3
+              run pmc_valu_c3 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/pmc1_c3" -o pmc --output-format csv -- $B3
+              run pmc_derived_c3 120 rocprofv3 --pmc VALUBusy VALUUtilization -d "$OUT/pmc4_c3" -o pmc --output-format csv -- $B3
+              run pmc_hbm_c3 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc2_c3" -o pmc --output-format csv -- $B3
+              run pmc_wr_c3 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc3_c3" -o pmc --output-format csv -- $B3 ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
 """Summarise a tools/gpu_session.sh prof+pmc run into profiles/ (committed evidence).
 
-  python tools/summarize_prof.py r01
+  python tools/summarize_prof.py r01          (config 2: dirs prof, pmc1..pmc4)
+  python tools/summarize_prof.py r01c3 _c3    (config 3: dirs prof_c3, pmc1_c3..pmc4_c3)
 writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
   profiles/<tag>_pmc_summary.json   per-kernel counters per launch (VALU, HBM bytes)
-  profiles/pmc_traffic.json         HBM bytes/launch per kernel, read by bench.py
+  profiles/pmc_traffic.json         HBM bytes/launch per kernel (config 2 run only)
+bench.py reads <tag>_pmc_summary.json of the config it runs (PMC_SUMMARY there).
 FETCH_SIZE is doubled: on gfx950 it reports half the bytes of a wide coalesced read
 (/opt/skills/guides/MI355X_MICROARCH.md, HBM section); both are in KB.
 """
@@ -41,9 +43,10 @@ def load_pmc(d):
 
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    sfx = sys.argv[2] if len(sys.argv) > 2 else ""
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
-    stats = os.path.join(OUT, "prof", "bench_kernel_stats.csv")
+    stats = os.path.join(OUT, "prof" + sfx, "bench_kernel_stats.csv")
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
     summary = {"tag": tag, "kernels": {}}
@@ -51,7 +54,7 @@ def main():
     merged = collections.defaultdict(dict)
     launches = {}
     for d in ("pmc1", "pmc2", "pmc3", "pmc4"):
-        v, n = load_pmc(d)
+        v, n = load_pmc(d + sfx)
         for k, cs in v.items():
             for c, x in cs.items():
                 merged[k][c] = x / max(n[k], 1)
@@ -71,7 +74,8 @@ def main():
                 e["int32_valu_fraction"] = cs["SQ_INSTS_VALU_INT32"] / cs["SQ_INSTS_VALU"]
         summary["kernels"][k] = e
     json.dump(summary, open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w"), indent=1)
-    json.dump(traffic, open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
+    if not sfx:
+        json.dump(traffic, open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(summary, indent=1)[:3000])
 
 
