@@ -337,6 +337,10 @@ def main() -> None:
                 # the guide's SIMD-32 nominal (2-cycle wave64 issue) rate: reachable only by
                 # streams without v_alignbit/v_add3, so not the bound here
                 "simd32_nominal_peak": round(VALU_PEAK_T * 2, 3),
+                "issued_frac_vs_simd32_nominal": round(kernel_ghs * issued_per_nonce / 1e3 / (VALU_PEAK_T * 2), 4) if issued_per_nonce else None,
+                "peak_basis": "SURVEY 8(d): 16 lanes/clk/SIMD at 2.4 GHz; measured ceiling of "
+                              "8-wave v_alignbit / v_bitop3 / SHA-mix streams 61-64 lane-instr/clk/CU "
+                              "(profiles/r01_valu_peak.jsonl, DESIGN 4.1)",
                 # shader clock over the dominant launches, from s_memtime / s_memrealtime
                 # in workgroup 0 (record the sustained sclk beside every GH/s)
                 "sclk_mhz": round(sclk, 1),
