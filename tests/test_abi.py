@@ -117,3 +117,56 @@ def test_plain_c_client_links_and_fails_loudly_without_gpu():
         pytest.skip("a GPU is visible: the no-device path is not reachable here")
     r = subprocess.run([CLI, "bradfitz", "0", "9999"], capture_output=True, text=True)
     assert r.returncode == 3 and "no usable gfx950" in r.stderr and r.stdout == ""
+
+
+def _split_args(s: str) -> list[str]:
+    """Top-level comma split of a call's argument text."""
+    out, depth, cur = [], 0, ""
+    for ch in s:
+        if ch in "([{":
+            depth += 1
+        elif ch in ")]}":
+            depth -= 1
+        if ch == "," and depth == 0:
+            out.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    if cur.strip():
+        out.append(cur.strip())
+    return out
+
+
+def _calls(src: str, prefix: str):
+    """(name, args) of every call `prefix<name>(...)` in src, balanced parentheses."""
+    for m in re.finditer(re.escape(prefix) + r"(gpuhash_[a-z_]+)\(", src):
+        i, depth = m.end(), 1
+        while depth:
+            depth += {"(": 1, ")": -1}.get(src[i], 0)
+            i += 1
+        yield m.group(1), _split_args(src[m.end():i - 1])
+
+
+def test_go_binding_matches_the_header():
+    # The cgo binding (integration/go) cannot be compiled here (no Go toolchain), so
+    # check it against include/gpuhash.h: every C.<name> it uses is declared, and every
+    # call passes as many arguments as the prototype takes.
+    hdr = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    protos = {}
+    for name, args in _calls(hdr, ""):
+        protos.setdefault(name, 0 if args == ["void"] else len(args))
+    go_dir = os.path.join(ROOT, "integration", "go")
+    srcs = [open(os.path.join(d, f)).read() for d, _, fs in os.walk(go_dir) for f in fs if f.endswith(".go")]
+    assert srcs
+    used = set()
+    for src in srcs:
+        used |= set(re.findall(r"\bC\.(gpuhash_\w+|GPUHASH_\w+)", src))
+        for name, args in _calls(src, "C."):
+            assert name in protos, name
+            assert len(args) == protos[name], (name, args, protos[name])
+    for ident in used:
+        if ident.startswith("GPUHASH_"):
+            assert re.search(r"\b" + ident + r"\b", hdr), ident
+        elif ident not in protos:  # a type, e.g. gpuhash_ctx
+            assert re.search(r"typedef\s+struct\s+" + ident + r"\b", hdr), ident
+    assert {"gpuhash_open", "gpuhash_min", "gpuhash_close"} <= used
