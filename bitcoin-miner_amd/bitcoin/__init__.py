@@ -15,7 +15,24 @@ import lsp
 from gpuhash import Hash, Message, MsgType, NewJoin, NewRequest, NewResult
 
 __all__ = ["Hash", "Message", "MsgType", "NewJoin", "NewRequest", "NewResult", "marshal",
-           "unmarshal", "params_from_env"]
+           "unmarshal", "params_from_env", "ParseUint", "UINT64_MAX", "EMPTY_RESULT"]
+
+UINT64_MAX = (1 << 64) - 1
+# (Hash, Nonce) of an empty range: the top of the lexicographic key order, so folding it
+# into any merge changes nothing (the identity of the (hash, nonce) min)
+EMPTY_RESULT = (UINT64_MAX, UINT64_MAX)
+
+
+def ParseUint(s: str) -> int:
+    """strconv.ParseUint(s, 10, 64) as Go's client would parse maxNonce: ASCII decimal
+    digits only (no sign, no spaces, no '_'), value <= 2^64-1; ValueError otherwise.
+    (Python's int() also accepts '+5', ' 5', '1_000' and negatives.)"""
+    if not s or not s.isascii() or not s.isdigit():
+        raise ValueError(f'strconv.ParseUint: parsing "{s}": invalid syntax')
+    v = int(s)
+    if v > UINT64_MAX:
+        raise ValueError(f'strconv.ParseUint: parsing "{s}": value out of range')
+    return v
 
 
 def marshal(m: Message) -> bytes:
@@ -23,11 +40,33 @@ def marshal(m: Message) -> bytes:
     return json.dumps(m.to_json(), separators=(",", ":")).encode()
 
 
+def _u64(d: dict, key: str) -> int:
+    """A uint64 field as Go's json.Unmarshal accepts it: an integer literal in
+    [0, 2^64-1] (no fraction, exponent or sign); anything else fails the whole message."""
+    v = d.get(key, 0)
+    if v is None:
+        return 0
+    if isinstance(v, bool) or not isinstance(v, int) or not 0 <= v <= UINT64_MAX:
+        raise ValueError(f"json: cannot unmarshal {v!r} into Go struct field Message.{key} of type uint64")
+    return v
+
+
 def unmarshal(raw: bytes) -> Message:
+    """json.Unmarshal into bitcoin.Message (message.go:16-21); raises ValueError where Go
+    would return an error, so callers drop the message as the reference would."""
     d = json.loads(raw)
-    return Message(MsgType(int(d.get("Type", 0))), Data=d.get("Data", "") or "",
-                   Lower=int(d.get("Lower", 0)), Upper=int(d.get("Upper", 0)),
-                   Hash=int(d.get("Hash", 0)), Nonce=int(d.get("Nonce", 0)))
+    if not isinstance(d, dict):
+        raise ValueError("json: cannot unmarshal non-object into Go value of type bitcoin.Message")
+    t = d.get("Type", 0)
+    if isinstance(t, bool) or not isinstance(t, int):
+        raise ValueError(f"json: cannot unmarshal {t!r} into Go struct field Message.Type")
+    data = d.get("Data", "")
+    if data is None:
+        data = ""
+    if not isinstance(data, str):
+        raise ValueError(f"json: cannot unmarshal {type(data).__name__} into Go struct field Message.Data of type string")
+    return Message(MsgType(t), Data=data, Lower=_u64(d, "Lower"), Upper=_u64(d, "Upper"),
+                   Hash=_u64(d, "Hash"), Nonce=_u64(d, "Nonce"))
 
 
 def params_from_env() -> lsp.Params:

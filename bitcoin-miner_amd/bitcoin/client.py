@@ -10,7 +10,7 @@ import sys
 
 import lsp
 
-from . import NewRequest, MsgType, marshal, params_from_env, unmarshal
+from . import UINT64_MAX, NewRequest, MsgType, ParseUint, marshal, params_from_env, unmarshal
 
 
 def printResult(hash_: str, nonce: str) -> None:  # client.go:19-21
@@ -23,6 +23,8 @@ def printDisconnected() -> None:  # client.go:24-26
 
 def request(hostport: str, message: str, max_nonce: int, params=None):
     """Returns (hash, nonce), or None when the connection to the server is lost."""
+    if isinstance(max_nonce, bool) or not isinstance(max_nonce, int) or not 0 <= max_nonce <= UINT64_MAX:
+        raise ValueError(f"maxNonce {max_nonce!r} outside [0, 2^64-1]")
     try:
         c = lsp.NewClient(hostport, params or params_from_env())
     except lsp.LSPError:
@@ -30,7 +32,10 @@ def request(hostport: str, message: str, max_nonce: int, params=None):
     try:
         c.Write(marshal(NewRequest(message, 0, max_nonce)))
         while True:
-            m = unmarshal(c.Read())
+            try:
+                m = unmarshal(c.Read())
+            except (ValueError, KeyError):
+                continue  # not a Message: ignored, as json.Unmarshal's error would be
             if m.Type == MsgType.Result:
                 return m.Hash, m.Nonce
     except lsp.LSPError:
@@ -45,7 +50,7 @@ def main(argv=None) -> int:
         print("Usage: ./client <hostport> <message> <maxNonce>")
         return 0
     try:
-        max_nonce = int(argv[3])
+        max_nonce = ParseUint(argv[3])  # a uint64, as strconv.ParseUint would have it
     except ValueError:
         print(f"{argv[3]} is not a number.")
         return 0

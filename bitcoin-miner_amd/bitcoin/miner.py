@@ -14,7 +14,11 @@ import sys
 
 import lsp
 
-from . import MsgType, NewJoin, NewResult, marshal, params_from_env, unmarshal
+from . import EMPTY_RESULT, MsgType, NewJoin, NewResult, marshal, params_from_env, unmarshal
+
+
+def _log(line: str) -> None:  # stderr only: the programs' stdout is graded (p1.pdf p.15)
+    print(f"miner: {line}", file=sys.stderr, flush=True)
 
 
 def open_engine():
@@ -42,12 +46,32 @@ def run(hostport: str, engine=None, params=None, on_client=None) -> int:
                 m = unmarshal(c.Read())
             except (ValueError, KeyError):
                 continue  # not a Message: ignore, like the server does
-            if m.Type != MsgType.Request or m.Lower > m.Upper:
+            if m.Type != MsgType.Request:
+                continue
+            if m.Lower > m.Upper:
+                # the spec'd loop runs zero times; answer with the min over the empty set
+                # (the top of the key order, a no-op in the server's merge) so the job
+                # does not stay in flight
+                c.Write(marshal(NewResult(*EMPTY_RESULT)))
                 continue
             # was: for n := m.Lower; n <= m.Upper; n++ { h := bitcoin.Hash(m.Data, n) ... }
-            # an engine error (no device, HIP failure) propagates: the miner exits and
-            # the server requeues the job on another miner (p1.pdf p.15)
-            h, n = engine.min(m.Data, m.Lower, m.Upper)
+            try:
+                h, n = engine.min(m.Data, m.Lower, m.Upper)
+            except (ValueError, TypeError) as e:
+                _log(f"job {m} skipped: {e}")
+                continue
+            except Exception as e:
+                if getattr(e, "is_argument_error", False):
+                    # deterministic (EINVAL/ETOOLONG): every miner would fail it the same
+                    # way, so it is skipped rather than exiting (which would requeue it
+                    # to the next miner); the server validates requests so that its own
+                    # jobs never get here
+                    _log(f"job {m} skipped: {e}")
+                    continue
+                # a device error (no device, HIP failure) propagates: the miner exits and
+                # the server requeues the job on another miner (p1.pdf p.15), at most
+                # server.MAX_REQUEUES times
+                raise
             c.Write(marshal(NewResult(h, n)))
             jobs += 1
     except lsp.LSPError:

@@ -15,7 +15,15 @@ at most one whenever requests have work queued.
 
 Failures (p1.pdf p.15): a lost miner's job goes back to the FRONT of its request's queue
 (and waits for a miner if none is left); a lost client's requests are dropped -- queued
-jobs are discarded, in-flight results are ignored when they arrive.
+jobs are discarded, in-flight results are ignored when they arrive.  A job whose miners
+keep dying (more than MAX_REQUEUES losses, e.g. a job that trips a device fault on every
+GPU) is not handed to miner after miner: its request is abandoned and the client's
+connection closed, so the client prints "Disconnected".
+
+Validation: a Request is accepted only if 0 <= Lower <= Upper <= 2^64-1 (the uint64
+fields are already range-checked by unmarshal, as Go's json.Unmarshal would) and its
+Data fits the engine (GPUHASH_MAX_MSG bytes).  Anything else is rejected by closing the
+client's connection: no job is cut and nothing is left in flight.
 
 Merging: results fold with the lexicographic (hash, nonce) key, so the answer is the
 same however the range is chunked (lowest nonce among equal hashes).
@@ -31,10 +39,25 @@ import sys
 from dataclasses import dataclass, field
 
 import lsp
+from gpuhash import GPUHASH_MAX_MSG  # a constant only: the server never loads the engine
 
-from . import MsgType, NewRequest, NewResult, marshal, params_from_env, unmarshal
+from . import UINT64_MAX, MsgType, NewRequest, NewResult, marshal, params_from_env, unmarshal
 
 DEFAULT_JOB_SIZE = 1 << 34
+MAX_REQUEUES = 3
+
+
+def request_error(data: str, lower: int, upper: int) -> str | None:
+    """Why a client Request cannot be served, or None if it can."""
+    for name, v in (("Lower", lower), ("Upper", upper)):
+        if isinstance(v, bool) or not isinstance(v, int) or not 0 <= v <= UINT64_MAX:
+            return f"{name}={v!r} outside [0, 2^64-1]"
+    if lower > upper:
+        return f"empty range: Lower {lower} > Upper {upper}"
+    n = len(data.encode())
+    if n > GPUHASH_MAX_MSG:
+        return f"Data is {n} bytes, over the engine's {GPUHASH_MAX_MSG}"
+    return None
 
 
 @dataclass
@@ -42,6 +65,7 @@ class Job:
     req_id: int
     lower: int
     upper: int
+    requeues: int = 0  # times a miner holding this job was lost
 
 
 @dataclass
@@ -84,11 +108,13 @@ def split_jobs(req_id: int, lower: int, upper: int, size: int):
 class Scheduler:
     """Pure bookkeeping (no I/O): tests drive it directly."""
 
-    def __init__(self, job_size: int = DEFAULT_JOB_SIZE):
+    def __init__(self, job_size: int = DEFAULT_JOB_SIZE, max_requeues: int = MAX_REQUEUES):
         self.job_size = job_size
+        self.max_requeues = max_requeues
         self.requests: dict[int, Request] = {}
         self.miners: dict[int, Job | None] = {}   # miner conn -> job in flight
         self.idle: collections.deque = collections.deque()
+        self.abandoned: collections.deque = collections.deque()  # clients to disconnect
         self._ids = itertools.count(1)
 
     def add_miner(self, conn: int) -> None:
@@ -97,6 +123,10 @@ class Scheduler:
             self.idle.append(conn)
 
     def add_request(self, client: int, data: str, lower: int, upper: int) -> int:
+        """Registers a request; ValueError (nothing registered) if request_error()."""
+        err = request_error(data, lower, upper)
+        if err is not None:
+            raise ValueError(err)
         rid = next(self._ids)
         r = Request(rid, client, data, next_lo=lower, upper=upper)
         self.requests[rid] = r
@@ -149,6 +179,13 @@ class Scheduler:
             if job is not None and job.req_id in self.requests:
                 r = self.requests[job.req_id]
                 r.inflight -= 1
+                job.requeues += 1
+                if job.requeues > self.max_requeues:
+                    # every miner that took this job died: stop feeding it to the rest
+                    del self.requests[r.req_id]
+                    self.abandoned.append(r.client)
+                    return (note + f"; job [{job.lower}, {job.upper}] lost {job.requeues} miners: "
+                            f"request {r.req_id} abandoned, client {r.client} disconnected")
                 r.requeued.appendleft(job)
                 note += f"; job [{job.lower}, {job.upper}] of request {job.req_id} requeued"
         dropped = [rid for rid, r in self.requests.items() if r.client == conn]
@@ -170,7 +207,16 @@ def serve(port: int, params=None, job_size: int | None = None, ready=None, log=N
         ready(srv)
     sched = Scheduler(job_size or int(os.environ.get("GPUHASH_JOB_SIZE", DEFAULT_JOB_SIZE)))
 
+    def disconnect_abandoned():
+        while sched.abandoned:
+            client = sched.abandoned.popleft()
+            try:
+                srv.CloseConn(client)
+            except lsp.LSPError:
+                pass
+
     def dispatch():
+        disconnect_abandoned()
         while True:
             a = sched.next_assignment()
             if a is None:
@@ -182,6 +228,7 @@ def serve(port: int, params=None, job_size: int | None = None, ready=None, log=N
                 note = sched.lost(miner)
                 if log and note:
                     log(note)
+                disconnect_abandoned()
 
     while True:
         try:
@@ -201,7 +248,16 @@ def serve(port: int, params=None, job_size: int | None = None, ready=None, log=N
         if m.Type == MsgType.Join:
             sched.add_miner(conn)
         elif m.Type == MsgType.Request:
-            sched.add_request(conn, m.Data, m.Lower, m.Upper)
+            try:
+                sched.add_request(conn, m.Data, m.Lower, m.Upper)
+            except ValueError as e:  # rejected: the client sees its connection close
+                if log:
+                    log(f"conn {conn}: request rejected ({e}); closing the connection")
+                try:
+                    srv.CloseConn(conn)
+                except lsp.LSPError:
+                    pass
+                continue
         elif m.Type == MsgType.Result:
             done = sched.result(conn, m.Hash, m.Nonce)
             if done is not None:

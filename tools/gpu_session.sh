@@ -8,6 +8,9 @@ cd "$(dirname "$0")/.."
 OUT=gpurun_out
 mkdir -p "$OUT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
+# the build id of the library this session runs (profiles are matched against it)
+python3 -c "import sys; sys.path.insert(0, 'bitcoin-miner_amd'); import gpuhash; print(gpuhash.build_id())" \
+    > "$OUT/build_id.txt" 2>/dev/null || echo unknown > "$OUT/build_id.txt"
 
 run() {  # run <name> <seconds> <cmd...>
     local name=$1 secs=$2

@@ -49,7 +49,11 @@ def main():
     stats = os.path.join(OUT, "prof" + sfx, "bench_kernel_stats.csv")
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
-    summary = {"tag": tag, "kernels": {}}
+    # build id of the library the box ran (tools/gpu_session.sh writes it at session
+    # start); bench.py uses these counters only while the library has the same id
+    bid_path = os.path.join(OUT, "build_id.txt")
+    build_id = open(bid_path).read().strip() if os.path.exists(bid_path) else None
+    summary = {"tag": tag, "build_id": build_id, "kernels": {}}
     traffic = {"source": f"profiles/{tag}_pmc_summary.json", "kernels": {}}
     merged = collections.defaultdict(dict)
     launches = {}
