@@ -351,7 +351,10 @@ def main() -> None:
                 "peak": round(VALU_PEAK_T, 3),
                 "unit": "T int32 lane-ops/s",
                 "frac": round(achieved_T / VALU_PEAK_T, 4),
-                "frac_basis": "algorithmic ops / the guide's SIMD-32 VALU peak (2-cycle wave64 issue)",
+                "frac_basis": "algorithmic ops / the guide's SIMD-32 VALU peak (2-cycle wave64 issue)"
+                              + ("; the algorithmic count charges c=2 blocks per nonce but this layout "
+                                 "compresses block B-1 once per lane row, so frac exceeds 1: issued_frac "
+                                 "is the hardware-bounded figure" if achieved_T > VALU_PEAK_T else ""),
                 "traffic": pmc_traffic(pmc),
                 "kernel": f"k_scan<J={key[0]},C2={key[1]},EX={key[2]},MODE=0>",
                 "avg_launch_ms": round(avg_ms, 4),

@@ -2,7 +2,7 @@
 # tools/gpu_session.sh STEP... -- runs GPU steps on the gpurun box, each under its own
 # time limit, logging to gpurun_out/.  A plain failure (exit 1, e.g. a failing test)
 # lets the next step run; a fault, abort, segfault, time limit or kill stops the session.
-# Steps: valu | go | test | smoke | bench | bench3 | bench4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | pmc3 | sweep | sys5
+# Steps: valu | go | test | soak | smoke | bench | bench3 | bench4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | pmc3 | sweep | sys5
 set -u
 cd "$(dirname "$0")/.."
 OUT=gpurun_out
@@ -44,6 +44,7 @@ for step in "$@"; do
         latency) run latency 120 python -u tools/latency.py ;;
         sweep) run sweep 600 python -u tools/layout_sweep.py ;;
         sys5) run sys5 900 python -u tools/system_bench.py ;;
+        soak) run soak 200 python -u tools/soak.py 90 "${SOAK_SEED:-2026}" ;;
         c4full) run c4full 400 python -u tools/config4_full.py ;;
         dist8c4) run dist8c4 400 env GPUHASH_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29547 bench.py --gpus 8 --config 4 --steps 1 --warmup 0 ;;
         bench3) run bench3 300 python -u bench.py --config 3 --steps 5 --warmup 1 ;;
