@@ -201,6 +201,34 @@ def test_errors_are_loud(engine):
         gpuhash.Engine([0, 99])
     with pytest.raises(gpuhash.GpuHashError):
         engine.hash_range(b"x", U64, 2)  # wraps past 2^64-1
+    assert e.value.is_argument_error
+    with pytest.raises(gpuhash.GpuHashError) as e:
+        engine.min(b"x" * (gpuhash.GPUHASH_MAX_MSG + 1), 0, 9)
+    assert e.value.rc == gpuhash.GPUHASH_ETOOLONG and e.value.is_argument_error
+    # bounds outside uint64 never reach ctypes (which would wrap 2^64+5 to 5)
+    with pytest.raises(ValueError):
+        engine.min(b"x", 0, U64 + 6)
+    with pytest.raises(ValueError):
+        engine.min(b"x", -1, 5)
+    # and the context is still usable after every refused call
+    assert engine.min(b"msg", 0, 2) == (4754799531757243342, 1)
+
+
+def test_calls_leave_the_current_device_alone(engine, oracle):
+    """Every entry point restores the calling thread's HIP device (include/gpuhash.h).
+    With one GPU only device 0 exists, so this checks the guard does not disturb it or
+    the torch-side current device across single- and multi-shard calls."""
+    import ctypes
+
+    import gpuhash
+    hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime libgpuhash.so links (same handle)
+    dev = ctypes.c_int(-1)
+    assert hip.hipSetDevice(0) == 0
+    with gpuhash.Engine([0, 0]) as two:
+        assert two.min(b"bradfitz", 0, 9999) == (1419516646206828, 9898)
+    engine.min(b"bradfitz", 0, 9999)
+    engine.hash_range(b"bradfitz", 0, 16)
+    assert hip.hipGetDevice(ctypes.byref(dev)) == 0 and dev.value == 0
 
 
 def test_multi_device_sharding_and_host_argmin(engine, oracle):
