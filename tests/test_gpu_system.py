@@ -76,6 +76,55 @@ def test_config1_end_to_end(procs):
     assert out.strip() == "Result 1419516646206828 9898", (out, err)
 
 
+NATIVE_MINER = os.path.join(ROOT, "bitcoin-miner_amd", "lib", "gpuhash_miner")
+
+
+def start_native(procs, port, **extra):
+    p = subprocess.Popen([NATIVE_MINER, f"127.0.0.1:{port}"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         text=True, env=env(**extra))
+    procs.ps.append(p)
+    return p
+
+
+def test_config1_with_the_compiled_miner(procs):
+    """The miner program in C++ (csrc/miner_main.cpp, linked to the product
+    libgpuhash.so) between the Python server and client."""
+    port = free_port()
+    procs.start([os.path.join(BIN, "server"), str(port)], env=env())
+    time.sleep(0.5)
+    start_native(procs, port)
+    c = procs.start([os.path.join(BIN, "client"), f"127.0.0.1:{port}", "bradfitz", "9999"], env=env())
+    out, err = c.communicate(timeout=90)
+    assert out.strip() == "Result 1419516646206828 9898", (out, err)
+
+
+def test_compiled_and_python_miners_together_with_drops_and_a_kill(procs, engine, oracle):
+    port = free_port()
+    drops = dict(LSPNET_CLIENT_READ_DROP=10, LSPNET_CLIENT_WRITE_DROP=10,
+                 LSPNET_SERVER_READ_DROP=10, LSPNET_SERVER_WRITE_DROP=10)
+    server = procs.start([os.path.join(BIN, "server"), str(port)],
+                         env=env(GPUHASH_JOB_SIZE=1 << 32, GPUHASH_SERVER_LOG=1, **drops))
+    time.sleep(0.5)
+    native = [start_native(procs, port, **drops) for _ in range(2)]
+    procs.start([os.path.join(BIN, "miner"), f"127.0.0.1:{port}"], env=env(**drops))
+    time.sleep(3.0)
+    max_nonce = 1 << 34
+    clients = [procs.start([os.path.join(BIN, "client"), f"127.0.0.1:{port}", f"native-{i:02d}",
+                            str(max_nonce)], env=env(**drops)) for i in range(6)]
+    time.sleep(1.5)
+    native[0].send_signal(signal.SIGKILL)  # mid-job: its job must be re-run elsewhere
+    for i, c in enumerate(clients):
+        parts = c.communicate(timeout=240)[0].split()
+        assert parts[0] == "Result", parts
+        h, n = int(parts[1]), int(parts[2])
+        msg = f"native-{i:02d}".encode()
+        assert (h, n) == engine.min(msg, 0, max_nonce), i
+        assert oracle.hash(msg, n) == h
+    server.send_signal(signal.SIGTERM)
+    log = server.communicate(timeout=30)[1]
+    assert "requeued" in log, log[-2000:]
+
+
 def test_client_prints_disconnected_without_server(procs):
     c = procs.start([os.path.join(BIN, "client"), f"127.0.0.1:{free_port()}", "bradfitz", "9999"],
                     env=env(LSP_EPOCH_MILLIS=100, LSP_EPOCH_LIMIT=3))

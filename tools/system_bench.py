@@ -7,6 +7,7 @@ itself parity-tested against the oracle) and re-hashes on the oracle.
 
   python tools/system_bench.py                       # config 5: 16 clients x 2^36, 8 miners
   python tools/system_bench.py --clients 4 --bits 32 --miners 2
+  python tools/system_bench.py --native                # miners = the compiled lib/gpuhash_miner
 """
 from __future__ import annotations
 
@@ -21,6 +22,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "bitcoin-miner_amd", "bin")
+NATIVE_MINER = os.path.join(ROOT, "bitcoin-miner_amd", "lib", "gpuhash_miner")
 sys.path.insert(0, os.path.join(ROOT, "bitcoin-miner_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
@@ -42,6 +44,8 @@ def main() -> None:
     ap.add_argument("--job-bits", type=int, default=34)
     ap.add_argument("--kill-after", type=float, default=3.0, help="SIGKILL one miner after s (<0: never)")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--native", action="store_true",
+                    help="miners are the compiled program (lib/gpuhash_miner) instead of bin/miner")
     args = ap.parse_args()
 
     env = dict(os.environ, LSP_EPOCH_MILLIS="500", LSP_EPOCH_LIMIT="10",
@@ -50,9 +54,9 @@ def main() -> None:
     port = free_port()
     procs = []
 
-    def start(argv, **kw):
-        p = subprocess.Popen([sys.executable] + argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                             text=True, **kw)
+    def start(argv, native=False, **kw):
+        p = subprocess.Popen(argv if native else [sys.executable] + argv, stdout=subprocess.PIPE,
+                             stderr=subprocess.PIPE, text=True, **kw)
         procs.append(p)
         return p
 
@@ -66,7 +70,10 @@ def main() -> None:
             e = dict(env)
             if ngpu:
                 e["GPUHASH_DEVICES"] = str(i % ngpu)
-            miners.append(start([os.path.join(BIN, "miner"), f"127.0.0.1:{port}"], env=e))
+            if args.native:
+                miners.append(start([NATIVE_MINER, f"127.0.0.1:{port}"], native=True, env=e))
+            else:
+                miners.append(start([os.path.join(BIN, "miner"), f"127.0.0.1:{port}"], env=e))
         time.sleep(5.0)  # miners open their GPU and join
         max_nonce = (1 << args.bits)
         t0 = time.perf_counter()
@@ -102,7 +109,8 @@ def main() -> None:
                     ok = ok and good
         total = args.clients * (max_nonce + 1)
         print(json.dumps({
-            "workload": f"config 5: {args.clients} clients x [0, 2^{args.bits}], {args.miners} GPU miners, "
+            "workload": f"config 5: {args.clients} clients x [0, 2^{args.bits}], {args.miners} GPU miners "
+                        f"({'lib/gpuhash_miner' if args.native else 'bin/miner'}), "
                         f"lspnet drop {args.drop}% on every role, job 2^{args.job_bits}, "
                         f"miner killed at {killed}s",
             "wall_s": round(wall, 3), "system_GHs": round(total / wall / 1e9, 3),
