@@ -29,26 +29,59 @@ P = lsp.Params(EpochLimit=20, EpochMillis=40, WindowSize=1)
 MINER_ENV = {"LSP_EPOCH_LIMIT": "20", "LSP_EPOCH_MILLIS": "40", "LSP_WINDOW_SIZE": "1"}
 
 
-@pytest.fixture(scope="module")
-def miner_bin(tmp_path_factory):
-    d = tmp_path_factory.mktemp("native_miner")
+_BUILDS = {}
+
+
+def build_miner(d, san=None):
+    """The miner program linked to the oracle-backed ABI shim; `san` adds host
+    sanitizers to the program's own code (the reference graders run `go test -race`;
+    SURVEY 5: sanitizers on the host code stand in for it)."""
+    key = san or "plain"
+    if key in _BUILDS:
+        return _BUILDS[key]
     objs = []
     for src in ("hash_oracle.c", "gpuhash_oracle_abi.c"):
-        o = str(d / (src + ".o"))
+        o = str(d / f"{key}_{src}.o")
         subprocess.check_call(["gcc", "-O2", "-c", "-I", os.path.join(ROOT, "include"),
                                os.path.join(ROOT, "oracle", src), "-o", o])
         objs.append(o)
-    exe = str(d / "miner_oracle")
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-I",
+    exe = str(d / f"miner_oracle_{key.replace(',', '_')}")
+    flags = ["-O2"] if san is None else ["-O1", "-g", "-fno-omit-frame-pointer", f"-fsanitize={san}",
+                                         "-fno-sanitize-recover=all"]
+    subprocess.check_call(["g++", *flags, "-std=c++17", "-Wall", "-Wextra", "-Werror", "-I",
                            os.path.join(ROOT, "include"),
                            os.path.join(ROOT, "bitcoin-miner_amd", "csrc", "miner_main.cpp"), *objs,
                            "-lpthread", "-o", exe])
+    _BUILDS[key] = exe
     return exe
+
+
+@pytest.fixture(scope="module")
+def build_dir(tmp_path_factory):
+    return tmp_path_factory.mktemp("native_miner")
+
+
+@pytest.fixture(scope="module")
+def miner_bin(build_dir):
+    return build_miner(build_dir)
+
+
+SANITIZERS = [None, "thread", "address,undefined"]
+SAN_MARKERS = ("ThreadSanitizer", "AddressSanitizer", "runtime error:", "LeakSanitizer")
+
+
+@pytest.fixture(params=SANITIZERS, ids=["plain", "tsan", "asan_ubsan"])
+def san_miners(request, build_dir):
+    m = Miners(build_miner(build_dir, request.param))
+    yield m
+    m.kill_all()
+    for err in m.errs:
+        assert not any(k in err for k in SAN_MARKERS), err[-3000:]
 
 
 class Miners:
     def __init__(self, exe):
-        self.exe, self.ps = exe, []
+        self.exe, self.ps, self.errs = exe, [], []
 
     def start(self, port, **env):
         e = dict(os.environ)
@@ -62,7 +95,15 @@ class Miners:
     def kill_all(self):
         for p in self.ps:
             if p.poll() is None:
-                p.kill()
+                p.terminate()
+                try:
+                    p.wait(5)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            try:
+                self.errs.append(p.stderr.read() if p.stderr and not p.stderr.closed else "")
+            except ValueError:
+                pass
             p.wait(10)
 
 
@@ -116,18 +157,18 @@ def test_no_server_exits_nonzero(miner_bin):
     assert r.returncode == 1 and r.stdout == ""
 
 
-def test_config1_shape(miners):
+def test_config1_shape(san_miners):
     srv = start_server(job_size=2500)
-    miners.start(srv.port)
+    san_miners.start(srv.port)
     assert bclient.request(f"127.0.0.1:{srv.port}", "bradfitz", 9999, P) == (1419516646206828, 9898)
     close_quietly(srv)
 
 
-def test_many_clients_with_drops_on_every_role(miners, oracle):
+def test_many_clients_with_drops_on_every_role(san_miners, oracle):
     import lspnet
     srv = start_server(job_size=3000)
     for _ in range(3):
-        miners.start(srv.port, LSPNET_CLIENT_READ_DROP=10, LSPNET_CLIENT_WRITE_DROP=10)
+        san_miners.start(srv.port, LSPNET_CLIENT_READ_DROP=10, LSPNET_CLIENT_WRITE_DROP=10)
     lspnet.SetReadDropPercent(10)
     lspnet.SetWriteDropPercent(10)
     results = {}
@@ -197,9 +238,9 @@ class BareServer:
         return bitcoin.unmarshal(self.srv.Read()[1])
 
 
-def test_empty_range_bad_json_and_unicode(miners, oracle):
+def test_empty_range_bad_json_and_unicode(san_miners, oracle):
     s = BareServer()
-    miners.start(s.srv.port)
+    san_miners.start(s.srv.port)
     conn = s.join()
     s.srv.Write(conn, bitcoin.marshal(bitcoin.NewRequest("msg", 5, 4)))
     r = s.result()
