@@ -3,10 +3,19 @@ pp.13-15: split each client Request into jobs, farm them to miners, merge the Re
 answer the client.
 
 Job chunking: the reference leaves "a suitable maximum job size"
-open.  With GPU miners at ~34 GH/s each, a job of 2^34 nonces is ~0.5 s of GPU time:
-big enough that per-job overhead (one LSP round trip + one gpuhash_min call, ~ms) is
-<1%, small enough that a killed miner loses half a second of work and 16 concurrent
-requests still spread over 8 miners.  GPUHASH_JOB_SIZE overrides it.
+open.  The server sizes each job for the miner that takes it, to last about
+JOB_SECONDS (0.5 s): long enough that per-job overhead (one LSP round trip + one
+gpuhash_min call, ~ms) is <1%, short enough that a killed miner loses half a second of
+work.  A miner's rate is learned from its own results (work and time of its recent jobs,
+halved at every new result, so it follows a GPU that other miners start sharing); its
+first job is a 2^22-nonce probe (~0.1 ms on one MI355X, ~0.4 s for a CPU miner).  So
+one MI355X miner gets jobs of about 2^34 nonces, a miner driving 8 GPUs eight times
+that, and a CPU miner (the reference's loop, ~10^7 nonces/s) a few million -- a fixed
+size would either idle GPUs or leave a request waiting minutes on a slow miner's job.  End game: no job is cut
+larger than the request's uncut remainder divided by the number of miners, so the last
+part of a request is spread over every miner instead of landing on a few.
+GPUHASH_JOB_SIZE (or serve(job_size=...)) switches to fixed-size jobs; GPUHASH_JOB_SECONDS
+sets the target duration.
 
 Scheduler (p1.pdf p.15, "balances loads across all requests"): an idle miner always
 gets the next job of the outstanding request that currently has the FEWEST jobs in
@@ -36,6 +45,7 @@ import collections
 import itertools
 import os
 import sys
+import time
 from dataclasses import dataclass, field
 
 import lsp
@@ -45,6 +55,33 @@ from . import UINT64_MAX, MsgType, NewRequest, NewResult, marshal, params_from_e
 
 DEFAULT_JOB_SIZE = 1 << 34
 MAX_REQUEUES = 3
+JOB_SECONDS = 0.5
+
+
+@dataclass
+class Sizing:
+    """Adaptive job sizing: a job lasts about `target_s` on the miner that takes it."""
+    target_s: float = JOB_SECONDS
+    probe: int = 1 << 22          # first job of a miner whose rate is unknown
+    min_job: int = 1 << 16
+    max_job: int = 1 << 40
+
+
+@dataclass
+class MinerRate:
+    """Work and time of a miner's recent jobs, both halved at every new result: the
+    rate is dominated by its long recent jobs, so the round trip of a short probe does
+    not drag it down, and it follows a GPU that other miners start sharing."""
+    work: float = 0.0
+    secs: float = 0.0
+
+    def add(self, n: int, dt: float) -> None:
+        self.work = 0.5 * self.work + n
+        self.secs = 0.5 * self.secs + max(dt, 1e-6)
+
+    @property
+    def rate(self) -> float:
+        return self.work / self.secs
 
 
 def request_error(data: str, lower: int, upper: int) -> str | None:
@@ -85,6 +122,10 @@ class Request:
     def has_pending(self) -> bool:
         return bool(self.requeued) or self.next_lo <= self.upper
 
+    def uncut(self) -> int:
+        """Nonces not yet cut into any job."""
+        return max(0, self.upper - self.next_lo + 1)
+
     def pop_job(self, size: int) -> Job:
         if self.requeued:
             return self.requeued.popleft()
@@ -106,11 +147,17 @@ def split_jobs(req_id: int, lower: int, upper: int, size: int):
 
 
 class Scheduler:
-    """Pure bookkeeping (no I/O): tests drive it directly."""
+    """Pure bookkeeping (no I/O): tests drive it directly.  `sizing` None = fixed jobs of
+    `job_size`; otherwise jobs are sized per miner (Sizing), timed with `clock`."""
 
-    def __init__(self, job_size: int = DEFAULT_JOB_SIZE, max_requeues: int = MAX_REQUEUES):
+    def __init__(self, job_size: int = DEFAULT_JOB_SIZE, max_requeues: int = MAX_REQUEUES,
+                 sizing: Sizing | None = None, clock=time.monotonic):
         self.job_size = job_size
         self.max_requeues = max_requeues
+        self.sizing = sizing
+        self.clock = clock
+        self.rates: dict[int, MinerRate] = {}
+        self.started: dict[int, float] = {}   # miner -> dispatch time of its job
         self.requests: dict[int, Request] = {}
         self.miners: dict[int, Job | None] = {}   # miner conn -> job in flight
         self.idle: collections.deque = collections.deque()
@@ -142,11 +189,29 @@ class Scheduler:
             miner = self.idle.popleft()
             if miner not in self.miners:
                 continue
-            job = r.pop_job(self.job_size)
+            job = r.pop_job(self.size_for(miner, r))
             r.inflight += 1
             self.miners[miner] = job
+            self.started[miner] = self.clock()
             return miner, job, r.data
         return None
+
+    def size_for(self, miner: int, r: Request) -> int:
+        """Nonces of the next job cut from `r` for `miner`."""
+        if self.sizing is None:
+            return self.job_size
+        s = self.sizing
+        mr = self.rates.get(miner)
+        if mr is None:
+            return s.probe
+        size = int(mr.rate * s.target_s)
+        # end game: what is left of the request is spread over its share of the miners
+        # (all of them when it is the only request with work left), down to a quarter of
+        # this miner's full job so the tail is not shredded into tiny jobs
+        active = sum(1 for x in self.requests.values() if x.has_pending())
+        miners = max(1, -(-len(self.miners) // max(1, active)))
+        share = max(-(-r.uncut() // miners), size // 4)
+        return max(s.min_job, min(s.max_job, size, share))
 
     def result(self, miner: int, h: int, n: int):
         """Folds a miner's result; returns (client, (hash, nonce)) when a request is done."""
@@ -155,6 +220,9 @@ class Scheduler:
             return None
         self.miners[miner] = None
         self.idle.append(miner)
+        t0 = self.started.pop(miner, None)
+        if t0 is not None:
+            self.rates.setdefault(miner, MinerRate()).add(job.upper - job.lower + 1, self.clock() - t0)
         r = self.requests.get(job.req_id)
         if r is None:  # the client is gone: ignore the result
             return None
@@ -171,6 +239,8 @@ class Scheduler:
         note = None
         if conn in self.miners:
             job = self.miners.pop(conn)
+            self.rates.pop(conn, None)
+            self.started.pop(conn, None)
             try:
                 self.idle.remove(conn)
             except ValueError:
@@ -205,7 +275,11 @@ def serve(port: int, params=None, job_size: int | None = None, ready=None, log=N
             print(f"server: {line}", file=sys.stderr, flush=True)
     if ready is not None:
         ready(srv)
-    sched = Scheduler(job_size or int(os.environ.get("GPUHASH_JOB_SIZE", DEFAULT_JOB_SIZE)))
+    fixed = job_size or int(os.environ.get("GPUHASH_JOB_SIZE", "0"))
+    if fixed:
+        sched = Scheduler(fixed)
+    else:
+        sched = Scheduler(sizing=Sizing(target_s=float(os.environ.get("GPUHASH_JOB_SECONDS", JOB_SECONDS))))
 
     def disconnect_abandoned():
         while sched.abandoned:
