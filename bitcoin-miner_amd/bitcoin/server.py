@@ -3,19 +3,23 @@ pp.13-15: split each client Request into jobs, farm them to miners, merge the Re
 answer the client.
 
 Job chunking: the reference leaves "a suitable maximum job size"
-open.  The server sizes each job for the miner that takes it, to last about
-JOB_SECONDS (0.5 s): long enough that per-job overhead (one LSP round trip + one
-gpuhash_min call, ~ms) is <1%, short enough that a killed miner loses half a second of
-work.  A miner's rate is learned from its own results (work and time of its recent jobs,
-halved at every new result, so it follows a GPU that other miners start sharing); its
-first job is a 2^22-nonce probe (~0.1 ms on one MI355X, ~0.4 s for a CPU miner).  So
-one MI355X miner gets jobs of about 2^34 nonces, a miner driving 8 GPUs eight times
-that, and a CPU miner (the reference's loop, ~10^7 nonces/s) a few million -- a fixed
-size would either idle GPUs or leave a request waiting minutes on a slow miner's job.  End game: no job is cut
-larger than the request's uncut remainder divided by the number of miners, so the last
-part of a request is spread over every miner instead of landing on a few.
-GPUHASH_JOB_SIZE (or serve(job_size=...)) switches to fixed-size jobs; GPUHASH_JOB_SECONDS
-sets the target duration.
+open.  Default: fixed jobs of 2^34 nonces, ~0.5 s on one MI355X -- big enough that the
+per-job overhead (one LSP round trip + one gpuhash_min call, ~ms, plus an epoch-long
+stall whenever a message is dropped) stays small, small enough that a killed miner
+loses half a second of work and 16 concurrent requests spread over 8 miners
+(GPUHASH_JOB_SIZE overrides the size).
+
+Per-miner sizing (GPUHASH_JOB_SECONDS=t, or Scheduler(sizing=Sizing(...))): each job is
+sized for the miner that takes it, to last ~t.  A miner's rate is learned from its own
+results (work and wall time of its recent jobs, halved at every new result); its first
+job is a 2^22-nonce probe.  This serves miners of
+very different speeds (a CPU miner running the reference loop next to MI355X miners: a
+2^34 job on it takes minutes) and spreads the end of a lone big request over every
+miner (no job larger than its uncut remainder over its share of the miners, down to a
+quarter job).  It is not the default because with lossy links its jobs, shorter than
+fixed 2^34 ones whenever miners share a GPU, pay more resend stalls: BASELINE config 5
+as run on a 1-GPU box (8 miners on one GPU, 10% drops) measured 29.6-30.9 GH/s against
+33.2-33.7 with fixed jobs.
 
 Scheduler (p1.pdf p.15, "balances loads across all requests"): an idle miner always
 gets the next job of the outstanding request that currently has the FEWEST jobs in
@@ -60,7 +64,7 @@ JOB_SECONDS = 0.5
 
 @dataclass
 class Sizing:
-    """Adaptive job sizing: a job lasts about `target_s` on the miner that takes it."""
+    """Per-miner job sizing: a job lasts about `target_s` on the miner that takes it."""
     target_s: float = JOB_SECONDS
     probe: int = 1 << 22          # first job of a miner whose rate is unknown
     min_job: int = 1 << 16
@@ -71,7 +75,9 @@ class Sizing:
 class MinerRate:
     """Work and time of a miner's recent jobs, both halved at every new result: the
     rate is dominated by its long recent jobs, so the round trip of a short probe does
-    not drag it down, and it follows a GPU that other miners start sharing."""
+    not drag it down, and it follows a GPU that other miners start sharing.  Time is
+    wall time per job, so the rate includes the job's round trip and any LSP resend
+    stall: a job then lasts ~target_s including them."""
     work: float = 0.0
     secs: float = 0.0
 
@@ -275,11 +281,11 @@ def serve(port: int, params=None, job_size: int | None = None, ready=None, log=N
             print(f"server: {line}", file=sys.stderr, flush=True)
     if ready is not None:
         ready(srv)
-    fixed = job_size or int(os.environ.get("GPUHASH_JOB_SIZE", "0"))
-    if fixed:
-        sched = Scheduler(fixed)
+    secs = os.environ.get("GPUHASH_JOB_SECONDS")
+    if job_size is None and secs:
+        sched = Scheduler(sizing=Sizing(target_s=float(secs)))
     else:
-        sched = Scheduler(sizing=Sizing(target_s=float(os.environ.get("GPUHASH_JOB_SECONDS", JOB_SECONDS))))
+        sched = Scheduler(job_size or int(os.environ.get("GPUHASH_JOB_SIZE", DEFAULT_JOB_SIZE)))
 
     def disconnect_abandoned():
         while sched.abandoned:

@@ -45,7 +45,7 @@ def main() -> None:
     ap.add_argument("--kill-after", type=float, default=3.0, help="SIGKILL one miner after s (<0: never)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--adaptive", action="store_true",
-                    help="the server sizes jobs per miner (its default) instead of fixed 2^job-bits jobs")
+                    help="the server sizes jobs per miner (GPUHASH_JOB_SECONDS=0.5) instead of fixed 2^job-bits jobs")
     ap.add_argument("--native", action="store_true",
                     help="miners are the compiled program (lib/gpuhash_miner) instead of bin/miner")
     args = ap.parse_args()
@@ -64,7 +64,9 @@ def main() -> None:
 
     try:
         senv = dict(env, GPUHASH_SERVER_LOG="1")
-        if not args.adaptive:
+        if args.adaptive:
+            senv["GPUHASH_JOB_SECONDS"] = "0.5"
+        else:
             senv["GPUHASH_JOB_SIZE"] = str(1 << args.job_bits)
         server = start([os.path.join(BIN, "server"), str(port)], env=senv)
         time.sleep(0.5)
@@ -116,7 +118,7 @@ def main() -> None:
             "workload": f"config 5: {args.clients} clients x [0, 2^{args.bits}], {args.miners} GPU miners "
                         f"({'lib/gpuhash_miner' if args.native else 'bin/miner'}), "
                         f"lspnet drop {args.drop}% on every role, "
-                        f"{'adaptive jobs (~0.5 s per miner)' if args.adaptive else f'job 2^{args.job_bits}'}, "
+                        f"{'per-miner jobs (~0.5 s)' if args.adaptive else f'job 2^{args.job_bits}'}, "
                         f"miner killed at {killed}s",
             "wall_s": round(wall, 3), "system_GHs": round(total / wall / 1e9, 3),
             "jobs_requeued": requeued, "all_results_verified": ok, "outputs": outs[:4],
