@@ -47,7 +47,7 @@ for step in "$@"; do
         sys5n) run sys5n 900 python -u tools/system_bench.py --native ;;
         sys5a) run sys5a 900 python -u tools/system_bench.py --adaptive
                run sys5an 900 python -u tools/system_bench.py --adaptive --native ;;
-        soak) run soak 200 python -u tools/soak.py 90 "${SOAK_SEED:-2026}" ;;
+        soak) run soak 400 python -u tools/soak.py "${SOAK_SECONDS:-90}" "${SOAK_SEED:-2026}" ;;
         c4full) run c4full 400 python -u tools/config4_full.py ;;
         dist8c4) run dist8c4 400 env GPUHASH_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29547 bench.py --gpus 8 --config 4 --steps 1 --warmup 0 ;;
         bench3) run bench3 300 python -u bench.py --config 3 --steps 5 --warmup 1 ;;
