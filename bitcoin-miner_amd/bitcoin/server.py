@@ -60,6 +60,7 @@ from . import UINT64_MAX, MsgType, NewRequest, NewResult, marshal, params_from_e
 DEFAULT_JOB_SIZE = 1 << 34
 MAX_REQUEUES = 3
 JOB_SECONDS = 0.5
+MINER_DEPTH = 2  # jobs a miner holds at once (serve(); GPUHASH_MINER_DEPTH overrides)
 
 
 @dataclass
@@ -109,6 +110,7 @@ class Job:
     lower: int
     upper: int
     requeues: int = 0  # times a miner holding this job was lost
+    sent: float = 0.0  # when it was last dispatched (Scheduler clock)
 
 
 @dataclass
@@ -154,26 +156,34 @@ def split_jobs(req_id: int, lower: int, upper: int, size: int):
 
 class Scheduler:
     """Pure bookkeeping (no I/O): tests drive it directly.  `sizing` None = fixed jobs of
-    `job_size`; otherwise jobs are sized per miner (Sizing), timed with `clock`."""
+    `job_size`; otherwise jobs are sized per miner (Sizing), timed with `clock`.
+
+    `depth` = jobs a miner may hold at once.  With 2, a miner's next Request is already
+    queued in its LSP connection while it computes, so the Result -> Request round trip
+    and any resend stall after a dropped message overlap the GPU's work instead of
+    idling it.  A miner answers its Requests in order over an in-order connection, so a
+    Result belongs to the oldest job the miner holds."""
 
     def __init__(self, job_size: int = DEFAULT_JOB_SIZE, max_requeues: int = MAX_REQUEUES,
-                 sizing: Sizing | None = None, clock=time.monotonic):
+                 sizing: Sizing | None = None, clock=time.monotonic, depth: int = 1):
         self.job_size = job_size
         self.max_requeues = max_requeues
         self.sizing = sizing
         self.clock = clock
+        self.depth = max(1, depth)
         self.rates: dict[int, MinerRate] = {}
-        self.started: dict[int, float] = {}   # miner -> dispatch time of its job
+        self.done_at: dict[int, float] = {}   # miner -> when its last result arrived
         self.requests: dict[int, Request] = {}
-        self.miners: dict[int, Job | None] = {}   # miner conn -> job in flight
-        self.idle: collections.deque = collections.deque()
+        self.miners: dict[int, collections.deque] = {}  # miner conn -> its jobs, oldest first
         self.abandoned: collections.deque = collections.deque()  # clients to disconnect
         self._ids = itertools.count(1)
+        self._tick = itertools.count()
+        self._turn: dict[int, int] = {}       # miner -> when it last got a job
 
     def add_miner(self, conn: int) -> None:
         if conn not in self.miners:
-            self.miners[conn] = None
-            self.idle.append(conn)
+            self.miners[conn] = collections.deque()
+            self._turn[conn] = next(self._tick)
 
     def add_request(self, client: int, data: str, lower: int, upper: int) -> int:
         """Registers a request; ValueError (nothing registered) if request_error()."""
@@ -186,21 +196,23 @@ class Scheduler:
         return rid
 
     def next_assignment(self):
-        """(miner, job, data) for the next dispatch, or None."""
-        while self.idle:
-            cands = [r for r in self.requests.values() if r.has_pending()]
-            if not cands:
-                return None
-            r = min(cands, key=lambda x: (x.inflight, x.req_id))
-            miner = self.idle.popleft()
-            if miner not in self.miners:
-                continue
-            job = r.pop_job(self.size_for(miner, r))
-            r.inflight += 1
-            self.miners[miner] = job
-            self.started[miner] = self.clock()
-            return miner, job, r.data
-        return None
+        """(miner, job, data) for the next dispatch, or None.  The miner holding the
+        fewest jobs goes first (then the one served longest ago); the request with the
+        fewest jobs in flight gets it (then the oldest)."""
+        free = [m for m, q in self.miners.items() if len(q) < self.depth]
+        if not free:
+            return None
+        cands = [r for r in self.requests.values() if r.has_pending()]
+        if not cands:
+            return None
+        miner = min(free, key=lambda m: (len(self.miners[m]), self._turn[m]))
+        r = min(cands, key=lambda x: (x.inflight, x.req_id))
+        job = r.pop_job(self.size_for(miner, r))
+        job.sent = self.clock()
+        r.inflight += 1
+        self.miners[miner].append(job)
+        self._turn[miner] = next(self._tick)
+        return miner, job, r.data
 
     def size_for(self, miner: int, r: Request) -> int:
         """Nonces of the next job cut from `r` for `miner`."""
@@ -220,15 +232,17 @@ class Scheduler:
         return max(s.min_job, min(s.max_job, size, share))
 
     def result(self, miner: int, h: int, n: int):
-        """Folds a miner's result; returns (client, (hash, nonce)) when a request is done."""
-        job = self.miners.get(miner)
-        if job is None:
+        """Folds a miner's result (for its oldest job); returns (client, (hash, nonce))
+        when a request is done."""
+        q = self.miners.get(miner)
+        if not q:
             return None
-        self.miners[miner] = None
-        self.idle.append(miner)
-        t0 = self.started.pop(miner, None)
-        if t0 is not None:
-            self.rates.setdefault(miner, MinerRate()).add(job.upper - job.lower + 1, self.clock() - t0)
+        job = q.popleft()
+        now = self.clock()
+        # the job computed from when it was sent or the miner's previous result came back
+        start = max(job.sent, self.done_at.get(miner, job.sent))
+        self.done_at[miner] = now
+        self.rates.setdefault(miner, MinerRate()).add(job.upper - job.lower + 1, now - start)
         r = self.requests.get(job.req_id)
         if r is None:  # the client is gone: ignore the result
             return None
@@ -244,26 +258,27 @@ class Scheduler:
         """Forgets a lost connection; returns a log line describing what changed."""
         note = None
         if conn in self.miners:
-            job = self.miners.pop(conn)
+            jobs = self.miners.pop(conn)
+            self._turn.pop(conn, None)
             self.rates.pop(conn, None)
-            self.started.pop(conn, None)
-            try:
-                self.idle.remove(conn)
-            except ValueError:
-                pass
-            note = f"miner {conn} lost"
-            if job is not None and job.req_id in self.requests:
-                r = self.requests[job.req_id]
+            self.done_at.pop(conn, None)
+            notes = [f"miner {conn} lost"]
+            for job in reversed(jobs):  # requeued oldest-first at the front
+                r = self.requests.get(job.req_id)
+                if r is None:
+                    continue
                 r.inflight -= 1
                 job.requeues += 1
                 if job.requeues > self.max_requeues:
                     # every miner that took this job died: stop feeding it to the rest
                     del self.requests[r.req_id]
                     self.abandoned.append(r.client)
-                    return (note + f"; job [{job.lower}, {job.upper}] lost {job.requeues} miners: "
-                            f"request {r.req_id} abandoned, client {r.client} disconnected")
+                    notes.append(f"job [{job.lower}, {job.upper}] lost {job.requeues} miners: "
+                                 f"request {r.req_id} abandoned, client {r.client} disconnected")
+                    continue
                 r.requeued.appendleft(job)
-                note += f"; job [{job.lower}, {job.upper}] of request {job.req_id} requeued"
+                notes.append(f"job [{job.lower}, {job.upper}] of request {job.req_id} requeued")
+            note = "; ".join(notes)
         dropped = [rid for rid, r in self.requests.items() if r.client == conn]
         for rid in dropped:
             del self.requests[rid]
@@ -282,10 +297,11 @@ def serve(port: int, params=None, job_size: int | None = None, ready=None, log=N
     if ready is not None:
         ready(srv)
     secs = os.environ.get("GPUHASH_JOB_SECONDS")
+    depth = int(os.environ.get("GPUHASH_MINER_DEPTH", MINER_DEPTH))
     if job_size is None and secs:
-        sched = Scheduler(sizing=Sizing(target_s=float(secs)))
+        sched = Scheduler(sizing=Sizing(target_s=float(secs)), depth=depth)
     else:
-        sched = Scheduler(job_size or int(os.environ.get("GPUHASH_JOB_SIZE", DEFAULT_JOB_SIZE)))
+        sched = Scheduler(job_size or int(os.environ.get("GPUHASH_JOB_SIZE", DEFAULT_JOB_SIZE)), depth=depth)
 
     def disconnect_abandoned():
         while sched.abandoned:

@@ -11,6 +11,7 @@ Rates: one MI355X = 34.6 GH/s (profiles/r02_bench_config2.json); a CPU miner run
 the reference loop on 16 cores = 0.08 GH/s (the bench's cpu_baseline_multicore).
 """
 import heapq
+import random
 
 import pytest
 
@@ -21,9 +22,23 @@ CPU = 0.08e9
 LATENCY = 0.002  # one LSP round trip + one gpuhash_min call
 
 
-def simulate(sched, rates, requests, latency=LATENCY):
+def leg(rng, drop, epoch, latency=LATENCY):
+    """One direction of a job's round trip over LSP: half the latency, plus, for each of
+    its two messages (Data, Ack) that lspnet drops, a wait for the next epoch's resend."""
+    t = latency / 2
+    for _ in range(2):
+        if rng.random() < drop:
+            t += rng.uniform(0, epoch)
+            while rng.random() < drop:
+                t += epoch
+    return t
+
+
+def simulate(sched, rates, requests, latency=LATENCY, drop=0.0, epoch=0.5, seed=1):
     """Runs `sched` until every request is answered; returns ({client: finish time},
-    {req: [(lo, hi), ...]}, number of jobs)."""
+    {req: [(lo, hi), ...]}, number of jobs).  A miner works its jobs in order (a job
+    waits for the previous one); each leg of a round trip may lose messages."""
+    rng = random.Random(seed)
     now = [0.0]
     sched.clock = lambda: now[0]
     for m in rates:
@@ -31,6 +46,7 @@ def simulate(sched, rates, requests, latency=LATENCY):
     for i, (lo, hi) in enumerate(requests):
         sched.add_request(client=1000 + i, data=f"r{i}", lower=lo, upper=hi)
     events, done, cuts, seq = [], {}, {}, 0
+    free_at = {m: 0.0 for m in rates}
 
     def dispatch():
         nonlocal seq
@@ -40,7 +56,9 @@ def simulate(sched, rates, requests, latency=LATENCY):
                 return
             m, job, data = a
             cuts.setdefault(data, []).append((job.lower, job.upper))
-            t = now[0] + (job.upper - job.lower + 1) / rates[m] + latency
+            start = max(now[0] + leg(rng, drop, epoch, latency), free_at[m])
+            free_at[m] = start + (job.upper - job.lower + 1) / rates[m]
+            t = free_at[m] + leg(rng, drop, epoch, latency)
             seq += 1
             heapq.heappush(events, (t, seq, m, job))
 
@@ -144,8 +162,47 @@ def test_lost_miner_forgets_its_rate_and_fixed_mode_is_unchanged():
     s.result(m, 1, job.lower)
     assert 1 in s.rates
     s.lost(1)
-    assert 1 not in s.rates and 1 not in s.started
+    assert 1 not in s.rates and 1 not in s.done_at
     f = fixed()
     f.add_miner(1)
     f.add_request(client=9, data="x", lower=0, upper=(1 << 40) - 1)
     assert f.next_assignment()[1].upper == (1 << 34) - 1
+
+
+def test_depth_two_hides_round_trips_and_resends():
+    """Two jobs per miner: the next Request waits in the miner's connection while it
+    computes.  Config 5's shape with 10% drops on every message and 0.5 s epochs (the
+    system bench's), on an 8-GPU node (one miner per GPU) and on one GPU shared by 8."""
+    reqs = [(0, (1 << 36) - 1)] * 16
+    total = 16 * (1 << 36)
+    for rates, gain in (({m: GPU for m in range(8)}, 1.10), ({m: GPU / 8 for m in range(8)}, 1.01)):
+        ghs = {}
+        for depth in (1, 2):
+            done, cuts, _ = simulate(bserver.Scheduler(job_size=1 << 34, depth=depth), rates, reqs,
+                                     drop=0.1, epoch=0.5)
+            assert all(tiles(cuts[f"r{i}"], 0, (1 << 36) - 1) for i in range(16))
+            ghs[depth] = total / max(done.values()) / 1e9
+        assert ghs[2] >= gain * ghs[1], ghs
+    # lossless: depth 2 costs nothing
+    rates = {m: GPU for m in range(8)}
+    d1 = max(simulate(bserver.Scheduler(job_size=1 << 34, depth=1), rates, reqs)[0].values())
+    d2 = max(simulate(bserver.Scheduler(job_size=1 << 34, depth=2), rates, reqs)[0].values())
+    assert d2 <= 1.005 * d1
+
+
+def test_depth_two_bookkeeping():
+    s = bserver.Scheduler(job_size=10, depth=2)
+    s.add_request(client=100, data="a", lower=0, upper=99)
+    s.add_miner(1)
+    s.add_miner(2)
+    got = [s.next_assignment() for _ in range(4)]
+    assert s.next_assignment() is None  # both miners hold two jobs
+    assert sorted(m for m, _, _ in got) == [1, 1, 2, 2]
+    first = [j for m, j, _ in got if m == 1]
+    assert s.result(1, 7, first[0].lower) is None  # a Result is the OLDEST job's
+    assert list(s.miners[1]) == [first[1]]
+    two = [j for m, j, _ in got if m == 2]
+    note = s.lost(2)  # both of its jobs go back, oldest first
+    assert note.count("requeued") == 2
+    r = next(iter(s.requests.values()))
+    assert list(r.requeued) == two and r.inflight == 1
