@@ -60,7 +60,7 @@ from . import UINT64_MAX, MsgType, NewRequest, NewResult, marshal, params_from_e
 DEFAULT_JOB_SIZE = 1 << 34
 MAX_REQUEUES = 3
 JOB_SECONDS = 0.5
-MINER_DEPTH = 2  # jobs a miner holds at once (serve(); GPUHASH_MINER_DEPTH overrides)
+MINER_DEPTH = 1  # jobs a miner holds at once (serve(); GPUHASH_MINER_DEPTH overrides)
 
 
 @dataclass
@@ -162,7 +162,10 @@ class Scheduler:
     queued in its LSP connection while it computes, so the Result -> Request round trip
     and any resend stall after a dropped message overlap the GPU's work instead of
     idling it.  A miner answers its Requests in order over an in-order connection, so a
-    Result belongs to the oldest job the miner holds."""
+    Result belongs to the oldest job the miner holds.  The default stays 1: on one GPU
+    shared by 8 miners a stalled miner's share goes to the others anyway, and config 5
+    measured no gain there (33.2 vs 32.2-33.2 GH/s, a killed miner then strands two
+    jobs); the gain is for one miner per GPU over lossy links."""
 
     def __init__(self, job_size: int = DEFAULT_JOB_SIZE, max_requeues: int = MAX_REQUEUES,
                  sizing: Sizing | None = None, clock=time.monotonic, depth: int = 1):
