@@ -56,48 +56,72 @@ CONFIGS = {
 }
 
 
-def cpu_baseline(seconds: float = 12.0) -> dict:
-    """Oracle C restatement of the reference miner loop (fresh format + SHA-256 per
-    nonce, strict '<'), single thread, on a bounded sample of the same workload: the
-    d=10 nonces at the top of config 2's range."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import hash_oracle as ho
-    c = ho.load_c_oracle()
-    n = 1 << 16
+def _time_min(fn, seconds: float, n0: int) -> tuple[int, int, float]:
+    """Times fn(lo, hi) on the top of config 2's range (the d=10 nonces), first on n0
+    nonces, then on a sample sized to take ~`seconds`; returns (lo, n, dt)."""
     t = time.perf_counter()
-    c.min(MSG, PER_GPU - n, PER_GPU - 1)
+    fn(PER_GPU - n0, PER_GPU - 1)
     dt = time.perf_counter() - t
-    n = max(n, int(n * seconds / max(dt, 1e-6)))
+    n = max(n0, int(n0 * seconds / max(dt, 1e-6)))
     lo = PER_GPU - n
     t = time.perf_counter()
-    c.min(MSG, lo, PER_GPU - 1)
-    dt = time.perf_counter() - t
+    fn(lo, PER_GPU - 1)
+    return lo, n, time.perf_counter() - t
+
+
+def _threads() -> int:
+    try:
+        return min(16, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        return min(16, os.cpu_count() or 1)
+
+
+def cpu_baseline(seconds: float = 12.0) -> dict:
+    """The reference miner loop (fresh "%s %d" buffer + SHA-256 per nonce, ascending,
+    strict '<') on one core, on a bounded sample of the same workload: the d=10 nonces
+    at the top of config 2's range.  SHA-256 is OpenSSL's (oracle/cpu_baseline.c; SHA-NI
+    where the host has it), the closest stand-in here for Go's assembly crypto/sha256;
+    without libcrypto it falls back to the plain-C oracle."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import hash_oracle as ho
+    b = ho.load_cpu_baseline()
+    if b.available():
+        lo, n, dt = _time_min(lambda a, z: b.min(MSG, a, z), seconds, 1 << 18)
+        what = "oracle/cpu_baseline.c (OpenSSL SHA-256 per nonce, as Go's asm crypto/sha256)"
+    else:
+        c = ho.load_c_oracle()
+        lo, n, dt = _time_min(lambda a, z: c.min(MSG, a, z), seconds, 1 << 16)
+        what = "oracle/hash_oracle.c (plain-C SHA-256; libcrypto unavailable)"
     return {"value": n / dt / 1e9, "unit": "GH/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/hash_oracle.c scan of bradfitz [{lo}, {PER_GPU - 1}] ({n} nonces, 10 digits), "
+            "sample": f"{what} scan of bradfitz [{lo}, {PER_GPU - 1}] ({n} nonces, 10 digits), "
                       f"{dt:.1f} s; reference Go miner unavailable (no Go toolchain)"}
 
 
-def cpu_baseline_multicore(seconds: float = 5.0) -> dict:
-    """The same loop over contiguous per-thread sub-ranges (the SURVEY's 'one goroutine
-    per core' variant), threads = this process's CPU share capped at 16."""
+def cpu_baseline_plain_c(seconds: float = 5.0) -> dict:
+    """The same loop with the oracle's plain-C SHA-256 (the checker), one core."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import hash_oracle as ho
     c = ho.load_c_oracle()
-    try:
-        threads = min(16, len(os.sched_getaffinity(0)))
-    except AttributeError:
-        threads = min(16, os.cpu_count() or 1)
-    n = 1 << 18
-    t = time.perf_counter()
-    c.min(MSG, PER_GPU - n, PER_GPU - 1, threads=threads)
-    dt = time.perf_counter() - t
-    n = max(n, int(n * seconds / max(dt, 1e-6)))
-    lo = PER_GPU - n
-    t = time.perf_counter()
-    c.min(MSG, lo, PER_GPU - 1, threads=threads)
-    dt = time.perf_counter() - t
+    lo, n, dt = _time_min(lambda a, z: c.min(MSG, a, z), seconds, 1 << 16)
+    return {"value": n / dt / 1e9, "unit": "GH/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/hash_oracle.c scan of bradfitz [{lo}, {PER_GPU - 1}] ({n} nonces), {dt:.1f} s"}
+
+
+def cpu_baseline_multicore(seconds: float = 5.0) -> dict:
+    """The loop over contiguous per-thread sub-ranges (the SURVEY's 'one goroutine per
+    core' variant), threads = this process's CPU share capped at 16, OpenSSL SHA-256."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import hash_oracle as ho
+    threads = _threads()
+    b = ho.load_cpu_baseline()
+    if b.available():
+        fn, what = (lambda a, z: b.min(MSG, a, z, threads=threads)), "cpu_baseline.c (OpenSSL SHA-256)"
+    else:
+        c = ho.load_c_oracle()
+        fn, what = (lambda a, z: c.min(MSG, a, z, threads=threads)), "oracle_min_mt (plain C)"
+    lo, n, dt = _time_min(fn, seconds, 1 << 20)
     return {"value": n / dt / 1e9, "unit": "GH/s", "cores": threads, "kind": "port",
-            "sample": f"oracle_min_mt over bradfitz [{lo}, {PER_GPU - 1}] ({n} nonces), {dt:.1f} s"}
+            "sample": f"{what} over bradfitz [{lo}, {PER_GPU - 1}] ({n} nonces), {dt:.1f} s"}
 
 
 # committed rocprofv3 PMC summary per bench config (tools/summarize_prof.py): each was
@@ -386,6 +410,7 @@ def main() -> None:
         if world == 1 and not args.no_cpu_baseline and args.config == "2":
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
             out["cpu_baseline_multicore"] = cpu_baseline_multicore(args.cpu_seconds / 2)
+            out["cpu_baseline_plain_c"] = cpu_baseline_plain_c(args.cpu_seconds / 4)
         emit(out)
     eng.close()
     if dist is not None:

@@ -54,12 +54,59 @@ def min_py(msg: bytes, lower: int, upper: int) -> tuple[int, int]:
 
 
 def build_c_oracle(force: bool = False) -> str:
-    """Compile hash_oracle.c with gcc (no GPU, no ROCm needed)."""
+    """Compile hash_oracle.c (and the bench's cpu_baseline.c) with gcc (no GPU, no ROCm
+    needed)."""
     src = os.path.join(HERE, "hash_oracle.c")
     if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
         os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
         subprocess.check_call(["gcc", "-O2", "-fPIC", "-shared", "-pthread", "-o", LIB_PATH, src])
+    build_cpu_baseline(force)
     return LIB_PATH
+
+
+BASELINE_PATH = os.path.join(HERE, "build", "libcpubaseline.so")
+
+
+def build_cpu_baseline(force: bool = False) -> str:
+    """oracle/cpu_baseline.c: the reference loop with OpenSSL's SHA-256 (bench only)."""
+    src = os.path.join(HERE, "cpu_baseline.c")
+    if force or not os.path.exists(BASELINE_PATH) or os.path.getmtime(BASELINE_PATH) < os.path.getmtime(src):
+        os.makedirs(os.path.dirname(BASELINE_PATH), exist_ok=True)
+        subprocess.check_call(["gcc", "-O2", "-fPIC", "-shared", "-pthread", "-o", BASELINE_PATH, src, "-ldl"])
+    return BASELINE_PATH
+
+
+class CpuBaseline:
+    """ctypes view of oracle/build/libcpubaseline.so (bench.py's cpu_baseline leg)."""
+
+    def __init__(self):
+        if not os.path.exists(BASELINE_PATH):
+            build_cpu_baseline()
+        self.lib = ctypes.CDLL(BASELINE_PATH)
+        u64, sz, p = ctypes.c_uint64, ctypes.c_size_t, ctypes.c_char_p
+        self.lib.baseline_available.restype = ctypes.c_int
+        self.lib.baseline_hash.restype = u64
+        self.lib.baseline_hash.argtypes = [p, sz, u64]
+        self.lib.baseline_min.restype = ctypes.c_int
+        self.lib.baseline_min.argtypes = [p, sz, u64, u64, ctypes.c_int, ctypes.POINTER(u64), ctypes.POINTER(u64)]
+
+    def available(self) -> bool:
+        return bool(self.lib.baseline_available())
+
+    def hash(self, msg: bytes, nonce: int) -> int:
+        return int(self.lib.baseline_hash(msg, len(msg), nonce))
+
+    def min(self, msg: bytes, lower: int, upper: int, threads: int = 1) -> tuple[int, int]:
+        h, n = ctypes.c_uint64(), ctypes.c_uint64()
+        rc = self.lib.baseline_min(msg, len(msg), lower, upper, threads, ctypes.byref(h), ctypes.byref(n))
+        if rc != 0:
+            raise ValueError(f"baseline_min rc={rc}")
+        return int(h.value), int(n.value)
+
+
+def load_cpu_baseline() -> CpuBaseline:
+    build_cpu_baseline()
+    return CpuBaseline()
 
 
 class COracle:

@@ -113,3 +113,21 @@ def test_c_sha256_fips_vectors(oracle, data, digest):
     oracle.lib.oracle_sha256.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p]
     oracle.lib.oracle_sha256(data, len(data), out)
     assert "".join(f"{w:08x}" for w in out) == digest
+
+
+def test_cpu_baseline_matches_the_oracle(oracle):
+    """bench.py's CPU baseline (oracle/cpu_baseline.c, OpenSSL SHA-256) computes the same
+    Hash and argmin as the checker: the KATs (p1.pdf p.12), config 1's answer, a range
+    across the 9->10 digit boundary, and its threaded merge."""
+    import hash_oracle as ho
+    b = ho.load_cpu_baseline()
+    if not b.available():
+        pytest.skip("no libcrypto on this host")
+    assert [b.hash(b"msg", n) for n in range(3)] == [13781283048668101583, 4754799531757243342,
+                                                     5611725180048225792]
+    assert b.min(b"bradfitz", 0, 9999) == (1419516646206828, 9898)
+    m = (b"The quick brown fox jumps over the lazy dog. " * 3)[:120]
+    assert b.min(m, 999_990_000, 1_000_010_000) == oracle.min(m, 999_990_000, 1_000_010_000)
+    assert b.min(b"bradfitz", 0, 200_000, threads=7) == oracle.min(b"bradfitz", 0, 200_000)
+    with pytest.raises(ValueError):
+        b.min(b"x", 5, 4)
