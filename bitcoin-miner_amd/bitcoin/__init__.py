@@ -35,9 +35,40 @@ def ParseUint(s: str) -> int:
     return v
 
 
+def go_json_string(s: str) -> str:
+    """A string as Go's encoding/json writes it (encodeState.string): \\" and \\\\, \\n \\r
+    \\t, other control characters as \\u00XX, <, > and & as \\u003c.. (HTML-safe), U+2028
+    and U+2029 as \\u2028/\\u2029, any other character as raw UTF-8, and what is not valid
+    UTF-8 (here: a lone surrogate) as U+FFFD."""
+    out = ['"']
+    for c in s:
+        o = ord(c)
+        if c == '"':
+            out.append('\\"')
+        elif c == "\\":
+            out.append("\\\\")
+        elif c == "\n":
+            out.append("\\n")
+        elif c == "\r":
+            out.append("\\r")
+        elif c == "\t":
+            out.append("\\t")
+        elif o < 0x20 or c in "<>&" or o in (0x2028, 0x2029):
+            out.append(f"\\u{o:04x}")
+        elif 0xD800 <= o < 0xE000:
+            out.append("\ufffd")
+        else:
+            out.append(c)
+    out.append('"')
+    return "".join(out)
+
+
 def marshal(m: Message) -> bytes:
-    """json.Marshal(bitcoin.Message) as Go writes it (field order of message.go:16-21)."""
-    return json.dumps(m.to_json(), separators=(",", ":")).encode()
+    """json.Marshal(bitcoin.Message) byte for byte as Go writes it: fields in the order
+    of message.go:16-21, no spaces, Data escaped as go_json_string."""
+    d = m.to_json()
+    return ("{" + ",".join(f'"{k}":' + (go_json_string(v) if k == "Data" else str(int(v)))
+                           for k, v in d.items()) + "}").encode()
 
 
 def _u64(d: dict, key: str) -> int:

@@ -281,3 +281,22 @@ def test_engine_hash_range_and_hash_refuse_bad_bounds():
 def test_argument_error_classification():
     assert _argument_error().is_argument_error
     assert not _device_error().is_argument_error
+
+
+# ---- wire format: json.Marshal(bitcoin.Message) byte for byte ----------------------------
+
+@pytest.mark.parametrize("msg,raw", [
+    (bitcoin.NewJoin(), b'{"Type":0,"Data":"","Lower":0,"Upper":0,"Hash":0,"Nonce":0}'),
+    (bitcoin.NewResult(U64, 7), b'{"Type":2,"Data":"","Lower":0,"Upper":0,"Hash":18446744073709551615,"Nonce":7}'),
+    # Go: HTML-safe escapes for < > &, raw UTF-8, \n \r \t short forms, other controls \u00XX
+    (bitcoin.NewRequest('a<b>&"c"\\é\n\r\t\x01\x08\x0c\x7f ', 0, 9),
+     b'{"Type":1,"Data":"a\\u003cb\\u003e\\u0026\\"c\\"\\\\\xc3\xa9\\n\\r\\t\\u0001\\u0008\\u000c\x7f\\u2028",'
+     b'"Lower":0,"Upper":9,"Hash":0,"Nonce":0}'),
+])
+def test_marshal_is_byte_exact_with_go(msg, raw):
+    assert bitcoin.marshal(msg) == raw
+    assert bitcoin.unmarshal(raw) == msg
+
+
+def test_marshal_replaces_invalid_utf8_like_go():
+    assert bitcoin.marshal(bitcoin.NewRequest("x\ud800y", 1, 2)).startswith(b'{"Type":1,"Data":"x\xef\xbf\xbdy"')
