@@ -2,7 +2,7 @@
 # tools/gpu_session.sh STEP... -- runs GPU steps on the gpurun box, each under its own
 # time limit, logging to gpurun_out/.  A plain failure (exit 1, e.g. a failing test)
 # lets the next step run; a fault, abort, segfault, time limit or kill stops the session.
-# Steps: valu | go | test | soak | smoke | bench | bench3 | bench4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | pmc3 | sweep | sys5
+# Steps: valu | go | test | soak | smoke | bench | bench3 | bench4 | prof4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | pmc3 | sweep | sys5
 set -u
 cd "$(dirname "$0")/.."
 OUT=gpurun_out
@@ -52,6 +52,7 @@ for step in "$@"; do
         dist8c4) run dist8c4 400 env GPUHASH_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29547 bench.py --gpus 8 --config 4 --steps 1 --warmup 0 ;;
         bench3) run bench3 300 python -u bench.py --config 3 --steps 5 --warmup 1 ;;
         bench4) run bench4 300 python -u bench.py --config 4 --steps 2 --warmup 1 ;;
+        prof4) run prof_c4 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c4" -o bench --output-format csv -- python3 bench.py --config 4 --steps 1 --warmup 1 --no-cpu-baseline ;;
         prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
         pmc) run pmc_valu 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/pmc1" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
              run pmc_derived 120 rocprofv3 --pmc VALUBusy VALUUtilization -d "$OUT/pmc4" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
