@@ -1,0 +1,75 @@
+// client_main.cpp -- the client program of the reference, compiled.
+//
+// The reference's client is a Go program whose body is a stub
+// (src/github.com/cmu440/bitcoin/client/client.go:8-16, "TODO: implement this!" at :15,
+// with printResult / printDisconnected at :19-26); p1.pdf p.14 specifies it: connect to
+// the server, send [Request message 0 maxNonce], print "Result minHash nonce" when the
+// answer arrives or "Disconnected" if the server is lost.  maxNonce is parsed as
+// strconv.ParseUint(s, 10, 64) would parse it.
+//
+//   gpuhash_client host:port message maxNonce
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "lsp_native.h"
+
+namespace {
+
+void printResult(uint64_t hash, uint64_t nonce) {  // client.go:19-21
+    std::printf("Result %llu %llu\n", (unsigned long long)hash, (unsigned long long)nonce);
+}
+
+void printDisconnected() { std::printf("Disconnected\n"); }  // client.go:24-26
+
+bool parse_uint(const std::string& s, uint64_t& out) {  // strconv.ParseUint(s, 10, 64)
+    if (s.empty() || s.size() > 20) return false;
+    unsigned __int128 v = 0;
+    for (char c : s) {
+        if (c < '0' || c > '9') return false;
+        v = v * 10 + (unsigned)(c - '0');
+    }
+    if (v > (unsigned __int128)lspn::kU64Max) return false;
+    out = (uint64_t)v;
+    return true;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc != 4) {  // client.go:9-13
+        std::printf("Usage: ./client <hostport> <message> <maxNonce>\n");
+        return 0;
+    }
+    uint64_t max_nonce;
+    if (!parse_uint(argv[3], max_nonce)) {
+        std::printf("%s is not a number.\n", argv[3]);
+        return 0;
+    }
+    lspn::Params params;
+    lspn::Client client(params);
+    if (!client.connect(argv[1])) {
+        printDisconnected();
+        return 0;
+    }
+    lspn::BtcMsg req;  // bitcoin.NewRequest(message, 0, maxNonce)
+    req.type = lspn::Request;
+    req.data = argv[2];
+    req.lower = 0;
+    req.upper = max_nonce;
+    if (!client.write(lspn::btc_marshal(req))) {
+        printDisconnected();
+        return 0;
+    }
+    std::string payload;
+    while (client.read(payload)) {
+        lspn::BtcMsg m;
+        if (!lspn::btc_unmarshal(payload, m) || m.type != lspn::Result) continue;
+        printResult(m.hash, m.nonce);
+        std::fflush(stdout);
+        client.close();
+        return 0;
+    }
+    printDisconnected();
+    return 0;
+}

@@ -1,0 +1,839 @@
+// lsp_native.h -- the reference's wire protocol in C++, shared by the compiled programs
+// (miner_main.cpp, server_main.cpp).  Header-only; no HIP, no gpuhash types.
+//
+//   * JSON as Go's encoding/json reads and writes the two message types: lsp.Message
+//     (lsp/message.go:17-22) and bitcoin.Message (bitcoin/message.go:16-21);
+//   * lspnet's UDP endpoints with per-role drop injection (lspnet/conn.go:34-113,
+//     staff.go:14-58), the percentages taken from LSPNET_{CLIENT,SERVER}_{READ,WRITE}_DROP
+//     like the Python programs;
+//   * LSP (p1.pdf pp.2-7): Connect/Ack handshake, per-direction sequence numbers from 1,
+//     sliding window of WindowSize unacknowledged messages, in-order delivery, and per
+//     epoch: resend unacked data, re-ack the last WindowSize messages received, Ack 0
+//     while no data has arrived, loss after EpochLimit silent epochs.  The same state
+//     machine as bitcoin-miner_amd/lsp/endpoint.py; client_api.go / server_api.go shape
+//     the APIs.  One background thread per endpoint owns the socket and the epochs, so
+//     heartbeats continue while the program's main thread blocks in a long search.
+#pragma once
+
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <utility>
+#include <vector>
+
+namespace lspn {
+
+constexpr uint64_t kU64Max = ~0ull;
+constexpr size_t kMaxDatagram = 2000;  // the reference reads into 2000-byte buffers (lspnet/conn.go:35)
+
+// ---------------------------------------------------------------------------------
+// JSON
+
+struct JVal {
+    enum Kind { Null, Bool, Num, Str } kind = Null;
+    std::string text;  // Str: the decoded UTF-8 bytes; Num: the literal
+    bool b = false;
+};
+
+inline void put_utf8(std::string& out, uint32_t cp) {
+    if (cp < 0x80) {
+        out += (char)cp;
+    } else if (cp < 0x800) {
+        out += (char)(0xC0 | (cp >> 6));
+        out += (char)(0x80 | (cp & 0x3F));
+    } else if (cp < 0x10000) {
+        out += (char)(0xE0 | (cp >> 12));
+        out += (char)(0x80 | ((cp >> 6) & 0x3F));
+        out += (char)(0x80 | (cp & 0x3F));
+    } else {
+        out += (char)(0xF0 | (cp >> 18));
+        out += (char)(0x80 | ((cp >> 12) & 0x3F));
+        out += (char)(0x80 | ((cp >> 6) & 0x3F));
+        out += (char)(0x80 | (cp & 0x3F));
+    }
+}
+
+// Length of the valid UTF-8 sequence at s[i] (code point in *cp), or 0 if invalid
+// (Go's utf8.DecodeRune: overlong forms, surrogates and > U+10FFFF are invalid).
+inline int utf8_seq(const std::string& s, size_t i, uint32_t* cp) {
+    const unsigned char c = (unsigned char)s[i];
+    int n;
+    uint32_t v, min;
+    if (c < 0x80) { *cp = c; return 1; }
+    if ((c & 0xE0) == 0xC0) { n = 2; v = c & 0x1F; min = 0x80; }
+    else if ((c & 0xF0) == 0xE0) { n = 3; v = c & 0x0F; min = 0x800; }
+    else if ((c & 0xF8) == 0xF0) { n = 4; v = c & 0x07; min = 0x10000; }
+    else return 0;
+    if (i + (size_t)n > s.size()) return 0;
+    for (int k = 1; k < n; k++) {
+        const unsigned char d = (unsigned char)s[i + (size_t)k];
+        if ((d & 0xC0) != 0x80) return 0;
+        v = (v << 6) | (d & 0x3F);
+    }
+    if (v < min || v > 0x10FFFF || (v >= 0xD800 && v < 0xE000)) return 0;
+    *cp = v;
+    return n;
+}
+
+class JsonReader {
+   public:
+    explicit JsonReader(const std::string& s) : s_(s) {}
+
+    // A single JSON object whose values are scalars; false if malformed.
+    bool object(std::map<std::string, JVal>& out) {
+        ws();
+        if (!eat('{')) return false;
+        ws();
+        if (eat('}')) return end();
+        for (;;) {
+            ws();
+            std::string key;
+            if (!string(key)) return false;
+            ws();
+            if (!eat(':')) return false;
+            ws();
+            JVal v;
+            if (!value(v)) return false;
+            out[key] = v;  // Go keeps the last duplicate too
+            ws();
+            if (eat(',')) continue;
+            if (eat('}')) return end();
+            return false;
+        }
+    }
+
+   private:
+    const std::string& s_;
+    size_t i_ = 0;
+
+    void ws() {
+        while (i_ < s_.size() && (s_[i_] == ' ' || s_[i_] == '\t' || s_[i_] == '\n' || s_[i_] == '\r')) i_++;
+    }
+    bool eat(char c) {
+        if (i_ < s_.size() && s_[i_] == c) { i_++; return true; }
+        return false;
+    }
+    bool end() { ws(); return i_ == s_.size(); }
+    bool lit(const char* w) {
+        size_t n = std::strlen(w);
+        if (s_.compare(i_, n, w) != 0) return false;
+        i_ += n;
+        return true;
+    }
+    int hex4() {
+        if (i_ + 4 > s_.size()) return -1;
+        int v = 0;
+        for (int k = 0; k < 4; k++) {
+            char c = s_[i_ + (size_t)k];
+            int d = (c >= '0' && c <= '9') ? c - '0' : (c >= 'a' && c <= 'f') ? c - 'a' + 10
+                    : (c >= 'A' && c <= 'F') ? c - 'A' + 10 : -1;
+            if (d < 0) return -1;
+            v = v * 16 + d;
+        }
+        i_ += 4;
+        return v;
+    }
+    // JSON string -> UTF-8 bytes.  As Go's decoder: broken surrogate escapes and raw
+    // bytes that are not valid UTF-8 become U+FFFD (one per invalid byte).
+    bool string(std::string& out) {
+        if (!eat('"')) return false;
+        while (i_ < s_.size()) {
+            unsigned char c = (unsigned char)s_[i_];
+            if (c == '"') { i_++; return true; }
+            if (c < 0x20) return false;
+            if (c >= 0x80) {
+                uint32_t cp;
+                int n = utf8_seq(s_, i_, &cp);
+                if (n) { out.append(s_, i_, (size_t)n); i_ += (size_t)n; }
+                else { put_utf8(out, 0xFFFD); i_++; }
+                continue;
+            }
+            i_++;
+            if (c != '\\') { out += (char)c; continue; }
+            if (i_ >= s_.size()) return false;
+            char e = s_[i_++];
+            switch (e) {
+                case '"': out += '"'; break;
+                case '\\': out += '\\'; break;
+                case '/': out += '/'; break;
+                case 'b': out += '\b'; break;
+                case 'f': out += '\f'; break;
+                case 'n': out += '\n'; break;
+                case 'r': out += '\r'; break;
+                case 't': out += '\t'; break;
+                case 'u': {
+                    int cp = hex4();
+                    if (cp < 0) return false;
+                    if (cp >= 0xD800 && cp < 0xDC00) {  // high surrogate: needs a low one
+                        size_t save = i_;
+                        if (lit("\\u")) {
+                            int lo = hex4();
+                            if (lo >= 0xDC00 && lo < 0xE000) {
+                                put_utf8(out, 0x10000u + (((uint32_t)cp - 0xD800u) << 10) + ((uint32_t)lo - 0xDC00u));
+                                break;
+                            }
+                        }
+                        i_ = save;
+                        put_utf8(out, 0xFFFD);
+                    } else if (cp >= 0xDC00 && cp < 0xE000) {
+                        put_utf8(out, 0xFFFD);
+                    } else {
+                        put_utf8(out, (uint32_t)cp);
+                    }
+                    break;
+                }
+                default: return false;
+            }
+        }
+        return false;
+    }
+    bool value(JVal& v) {
+        if (i_ >= s_.size()) return false;
+        char c = s_[i_];
+        if (c == '"') { v.kind = JVal::Str; return string(v.text); }
+        if (lit("null")) { v.kind = JVal::Null; return true; }
+        if (lit("true")) { v.kind = JVal::Bool; v.b = true; return true; }
+        if (lit("false")) { v.kind = JVal::Bool; v.b = false; return true; }
+        if (c == '-' || (c >= '0' && c <= '9')) {
+            size_t b = i_;
+            if (c == '-') i_++;
+            while (i_ < s_.size() && std::strchr("0123456789.eE+-", s_[i_])) i_++;
+            v.kind = JVal::Num;
+            v.text = s_.substr(b, i_ - b);
+            return true;
+        }
+        return false;  // nested objects/arrays never appear in these messages
+    }
+};
+
+// A uint64 struct field as Go's json.Unmarshal fills it: a plain non-negative integer
+// literal <= 2^64-1; null (or absent) leaves the zero value.  Anything else fails.
+inline bool get_u64(const std::map<std::string, JVal>& o, const char* k, uint64_t& out) {
+    out = 0;
+    auto it = o.find(k);
+    if (it == o.end() || it->second.kind == JVal::Null) return true;
+    if (it->second.kind != JVal::Num) return false;
+    const std::string& t = it->second.text;
+    if (t.empty() || t.size() > 20) return false;
+    unsigned __int128 v = 0;
+    for (char c : t) {
+        if (c < '0' || c > '9') return false;
+        v = v * 10 + (unsigned)(c - '0');
+    }
+    if (t.size() > 1 && t[0] == '0') return false;  // not a JSON number
+    if (v > (unsigned __int128)kU64Max) return false;
+    out = (uint64_t)v;
+    return true;
+}
+
+inline bool get_int(const std::map<std::string, JVal>& o, const char* k, long long& out) {
+    out = 0;
+    auto it = o.find(k);
+    if (it == o.end() || it->second.kind == JVal::Null) return true;
+    if (it->second.kind != JVal::Num) return false;
+    const std::string& t = it->second.text;
+    size_t p = t[0] == '-' ? 1 : 0;
+    if (p >= t.size() || t.size() - p > 18) return false;
+    long long v = 0;
+    for (size_t i = p; i < t.size(); i++) {
+        if (t[i] < '0' || t[i] > '9') return false;
+        v = v * 10 + (t[i] - '0');
+    }
+    out = p ? -v : v;
+    return true;
+}
+
+// A string as Go's encoding/json writes it (encodeState.string): \" \\ \n \r \t, other
+// control characters as \u00XX, < > & as < > &, U+2028/U+2029 escaped,
+// other valid UTF-8 raw, invalid bytes as U+FFFD.
+inline std::string go_json_string(const std::string& s) {
+    static const char hex[] = "0123456789abcdef";
+    std::string out = "\"";
+    for (size_t i = 0; i < s.size();) {
+        const unsigned char c = (unsigned char)s[i];
+        if (c < 0x80) {
+            switch (c) {
+                case '"': out += "\\\""; break;
+                case '\\': out += "\\\\"; break;
+                case '\n': out += "\\n"; break;
+                case '\r': out += "\\r"; break;
+                case '\t': out += "\\t"; break;
+                default:
+                    if (c < 0x20 || c == '<' || c == '>' || c == '&') {
+                        out += "\\u00";
+                        out += hex[c >> 4];
+                        out += hex[c & 15];
+                    } else {
+                        out += (char)c;
+                    }
+            }
+            i++;
+            continue;
+        }
+        uint32_t cp;
+        int n = utf8_seq(s, i, &cp);
+        if (!n) {
+            out += "\xEF\xBF\xBD";
+            i++;
+        } else if (cp == 0x2028 || cp == 0x2029) {
+            out += cp == 0x2028 ? "\\u2028" : "\\u2029";
+            i += (size_t)n;
+        } else {
+            out.append(s, i, (size_t)n);
+            i += (size_t)n;
+        }
+    }
+    return out + "\"";
+}
+
+// ---------------------------------------------------------------------------------
+// base64 (Go's StdEncoding, padded): lsp.Message.Payload is a []byte.
+
+inline const char* b64_alphabet() { return "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/"; }
+
+inline std::string b64encode(const std::string& in) {
+    const char* A = b64_alphabet();
+    std::string out;
+    size_t i = 0;
+    for (; i + 3 <= in.size(); i += 3) {
+        uint32_t v = ((uint32_t)(uint8_t)in[i] << 16) | ((uint32_t)(uint8_t)in[i + 1] << 8) | (uint8_t)in[i + 2];
+        out += A[v >> 18]; out += A[(v >> 12) & 63]; out += A[(v >> 6) & 63]; out += A[v & 63];
+    }
+    if (in.size() - i == 1) {
+        uint32_t v = (uint32_t)(uint8_t)in[i] << 16;
+        out += A[v >> 18]; out += A[(v >> 12) & 63]; out += "==";
+    } else if (in.size() - i == 2) {
+        uint32_t v = ((uint32_t)(uint8_t)in[i] << 16) | ((uint32_t)(uint8_t)in[i + 1] << 8);
+        out += A[v >> 18]; out += A[(v >> 12) & 63]; out += A[(v >> 6) & 63]; out += '=';
+    }
+    return out;
+}
+
+inline bool b64decode(const std::string& in, std::string& out) {
+    const char* A = b64_alphabet();
+    if (in.size() % 4) return false;
+    out.clear();
+    for (size_t i = 0; i < in.size(); i += 4) {
+        int v[4];
+        int pad = 0;
+        for (int k = 0; k < 4; k++) {
+            char c = in[i + (size_t)k];
+            const char* p = c ? std::strchr(A, c) : nullptr;
+            if (c == '=' && i + 4 == in.size() && k >= 2) { v[k] = 0; pad++; continue; }
+            if (!p || pad) return false;
+            v[k] = (int)(p - A);
+        }
+        uint32_t x = ((uint32_t)v[0] << 18) | ((uint32_t)v[1] << 12) | ((uint32_t)v[2] << 6) | (uint32_t)v[3];
+        out += (char)(x >> 16);
+        if (pad < 2) out += (char)((x >> 8) & 0xFF);
+        if (pad < 1) out += (char)(x & 0xFF);
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------------------------
+// LSP wire messages (lsp/message.go:8-22)
+
+enum LspType { MsgConnect = 0, MsgData = 1, MsgAck = 2 };
+
+struct LspMsg {
+    long long type = 0, conn = 0, seq = 0;
+    bool has_payload = false;
+    std::string payload;
+};
+
+inline std::string lsp_marshal(const LspMsg& m) {
+    std::string s = "{\"Type\":" + std::to_string(m.type) + ",\"ConnID\":" + std::to_string(m.conn) +
+                    ",\"SeqNum\":" + std::to_string(m.seq) + ",\"Payload\":";
+    s += m.has_payload ? "\"" + b64encode(m.payload) + "\"" : std::string("null");
+    return s + "}";
+}
+
+inline bool lsp_unmarshal(const std::string& raw, LspMsg& m) {
+    std::map<std::string, JVal> o;
+    if (!JsonReader(raw).object(o)) return false;
+    if (!get_int(o, "Type", m.type) || !get_int(o, "ConnID", m.conn) || !get_int(o, "SeqNum", m.seq)) return false;
+    auto it = o.find("Payload");
+    m.has_payload = it != o.end() && it->second.kind == JVal::Str;
+    if (it != o.end() && it->second.kind != JVal::Str && it->second.kind != JVal::Null) return false;
+    if (m.has_payload && !b64decode(it->second.text, m.payload)) return false;
+    return true;
+}
+
+// ---------------------------------------------------------------------------------
+// bitcoin.Message (bitcoin/message.go:8-21)
+
+enum BtcType { Join = 0, Request = 1, Result = 2 };
+
+struct BtcMsg {
+    long long type = 0;
+    std::string data;
+    uint64_t lower = 0, upper = 0, hash = 0, nonce = 0;
+};
+
+inline bool btc_unmarshal(const std::string& raw, BtcMsg& m) {
+    std::map<std::string, JVal> o;
+    if (!JsonReader(raw).object(o)) return false;
+    if (!get_int(o, "Type", m.type)) return false;
+    auto it = o.find("Data");
+    if (it != o.end()) {
+        if (it->second.kind == JVal::Str) m.data = it->second.text;
+        else if (it->second.kind != JVal::Null) return false;
+    }
+    return get_u64(o, "Lower", m.lower) && get_u64(o, "Upper", m.upper) && get_u64(o, "Hash", m.hash) &&
+           get_u64(o, "Nonce", m.nonce);
+}
+
+// json.Marshal(bitcoin.Message), byte for byte as Go writes it
+inline std::string btc_marshal(const BtcMsg& m) {
+    return "{\"Type\":" + std::to_string(m.type) + ",\"Data\":" + go_json_string(m.data) +
+           ",\"Lower\":" + std::to_string(m.lower) + ",\"Upper\":" + std::to_string(m.upper) +
+           ",\"Hash\":" + std::to_string(m.hash) + ",\"Nonce\":" + std::to_string(m.nonce) + "}";
+}
+
+inline std::string btc_describe(const BtcMsg& m) {  // Message.String, message.go:49-60
+    switch (m.type) {
+        case Request:
+            return "[Request " + (m.data.size() > 40 ? m.data.substr(0, 40) + "..." : m.data) + " " +
+                   std::to_string(m.lower) + " " + std::to_string(m.upper) + "]";
+        case Result: return "[Result " + std::to_string(m.hash) + " " + std::to_string(m.nonce) + "]";
+        default: return "[Join]";
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// lspnet: UDP with per-role drop injection
+
+inline int env_int(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return e && *e ? std::atoi(e) : dflt;
+}
+
+struct Params {  // lsp/params.go:8-35, with the env overrides of bitcoin.params_from_env
+    int epoch_limit = env_int("LSP_EPOCH_LIMIT", 5);
+    int epoch_ms = env_int("LSP_EPOCH_MILLIS", 2000);
+    int window = env_int("LSP_WINDOW_SIZE", 1);
+};
+
+using Addr = std::pair<uint32_t, uint16_t>;  // IPv4 address and port, network order
+
+class Udp {
+   public:
+    explicit Udp(bool server)
+        : rdrop_(env_int(server ? "LSPNET_SERVER_READ_DROP" : "LSPNET_CLIENT_READ_DROP", 0)),
+          wdrop_(env_int(server ? "LSPNET_SERVER_WRITE_DROP" : "LSPNET_CLIENT_WRITE_DROP", 0)) {}
+    ~Udp() {
+        if (fd_ >= 0) close(fd_);
+    }
+    Udp(const Udp&) = delete;
+    Udp& operator=(const Udp&) = delete;
+
+    // client role: a socket aimed at host:port
+    bool dial(const std::string& hostport) {
+        size_t c = hostport.rfind(':');
+        if (c == std::string::npos) return false;
+        std::string host = hostport.substr(0, c), port = hostport.substr(c + 1);
+        if (host.empty()) host = "127.0.0.1";
+        addrinfo hints{}, *res = nullptr;
+        hints.ai_family = AF_INET;
+        hints.ai_socktype = SOCK_DGRAM;
+        if (getaddrinfo(host.c_str(), port.c_str(), &hints, &res) != 0 || !res) return false;
+        sockaddr_in a{};
+        std::memcpy(&a, res->ai_addr, sizeof a);
+        freeaddrinfo(res);
+        peer_ = Addr{a.sin_addr.s_addr, a.sin_port};
+        fd_ = socket(AF_INET, SOCK_DGRAM, 0);
+        return fd_ >= 0;
+    }
+    // server role: a socket bound to the port on every interface (0 = any free port)
+    bool listen(int port) {
+        fd_ = socket(AF_INET, SOCK_DGRAM, 0);
+        if (fd_ < 0) return false;
+        sockaddr_in a{};
+        a.sin_family = AF_INET;
+        a.sin_addr.s_addr = htonl(INADDR_ANY);
+        a.sin_port = htons((uint16_t)port);
+        if (bind(fd_, reinterpret_cast<sockaddr*>(&a), sizeof a) != 0) return false;
+        socklen_t l = sizeof a;
+        getsockname(fd_, reinterpret_cast<sockaddr*>(&a), &l);
+        port_ = ntohs(a.sin_port);
+        return true;
+    }
+    int fd() const { return fd_; }
+    int port() const { return port_; }
+    const Addr& peer() const { return peer_; }
+
+    void write(const std::string& data, const Addr& to) {
+        if (drop(wdrop_)) return;
+        sockaddr_in a{};
+        a.sin_family = AF_INET;
+        a.sin_addr.s_addr = to.first;
+        a.sin_port = to.second;
+        sendto(fd_, data.data(), data.size(), 0, reinterpret_cast<const sockaddr*>(&a), sizeof a);
+    }
+    // one ready datagram (and its sender); false if none is ready or the injector ate it
+    bool read(std::string& out, Addr& from) {
+        char buf[kMaxDatagram];
+        for (;;) {
+            sockaddr_in a{};
+            socklen_t l = sizeof a;
+            ssize_t n = recvfrom(fd_, buf, sizeof buf, MSG_DONTWAIT, reinterpret_cast<sockaddr*>(&a), &l);
+            if (n < 0) return false;
+            if (drop(rdrop_)) continue;  // eaten by the injector: try the next datagram
+            out.assign(buf, (size_t)n);
+            from = Addr{a.sin_addr.s_addr, a.sin_port};
+            return true;
+        }
+    }
+
+   private:
+    int fd_ = -1, port_ = 0;
+    Addr peer_{0, 0};
+    int rdrop_, wdrop_;
+    std::mt19937 rng_{std::random_device{}()};
+    bool drop(int pct) { return pct > 0 && (int)(rng_() % 100u) < pct; }
+};
+
+// ---------------------------------------------------------------------------------
+// One side of one connection (p1.pdf pp.4-7); the owner serialises all calls.
+
+class Conn {
+   public:
+    Conn(long long id, const Params& p, std::function<void(const LspMsg&)> send)
+        : id_(id), w_(std::max(1, p.window)), k_(std::max(1, p.epoch_limit)), send_(std::move(send)) {}
+
+    long long id() const { return id_; }
+    bool lost() const { return lost_; }
+    bool closing = false;
+    bool flushed() const { return pending_.empty() && unacked_.empty(); }
+
+    void write(std::string payload) {
+        pending_.emplace_back(next_seq_++, std::move(payload));
+        pump();
+    }
+
+    // a message from the peer; payloads that became deliverable in order go to `out`
+    void on_message(const LspMsg& m, std::deque<std::string>& out) {
+        silent_ = 0;
+        if (m.type == MsgAck) {
+            if (unacked_.erase(m.seq)) pump();
+            return;
+        }
+        if (m.type != MsgData) return;
+        send_(LspMsg{MsgAck, id_, m.seq, false, {}});
+        if (m.seq >= expected_ && m.seq < expected_ + w_ && !rbuf_.count(m.seq)) {
+            rbuf_.emplace(m.seq, m.payload);
+            recent_.push_back(m.seq);
+            if ((int)recent_.size() > w_) recent_.pop_front();
+            got_data_ = true;
+            for (auto it = rbuf_.find(expected_); it != rbuf_.end(); it = rbuf_.find(expected_)) {
+                out.push_back(std::move(it->second));
+                rbuf_.erase(it);
+                expected_++;
+            }
+        }
+    }
+
+    // epoch actions; true when this epoch made the connection lost
+    bool on_epoch() {
+        if (lost_) return false;
+        if (++silent_ >= k_) {
+            lost_ = true;
+            return true;
+        }
+        if (!got_data_) send_(LspMsg{MsgAck, id_, 0, false, {}});
+        for (auto& [seq, payload] : unacked_) send_(LspMsg{MsgData, id_, seq, true, payload});
+        for (long long seq : recent_) send_(LspMsg{MsgAck, id_, seq, false, {}});
+        return false;
+    }
+    void heard() { silent_ = 0; }
+
+   private:
+    long long id_;
+    int w_, k_;
+    std::function<void(const LspMsg&)> send_;
+    bool lost_ = false, got_data_ = false;
+    int silent_ = 0;
+    long long next_seq_ = 1, expected_ = 1;
+    std::deque<std::pair<long long, std::string>> pending_;  // not yet inside the window
+    std::map<long long, std::string> unacked_;               // sent, not acknowledged
+    std::map<long long, std::string> rbuf_;                  // received out of order
+    std::deque<long long> recent_;                           // last w distinct received seqs
+
+    long long window_base() const {
+        if (!unacked_.empty()) return unacked_.begin()->first;
+        if (!pending_.empty()) return pending_.front().first;
+        return next_seq_;
+    }
+    void pump() {
+        const long long base = window_base();
+        while (!pending_.empty() && pending_.front().first < base + w_) {
+            auto [seq, payload] = std::move(pending_.front());
+            pending_.pop_front();
+            send_(LspMsg{MsgData, id_, seq, true, payload});
+            unacked_.emplace(seq, std::move(payload));
+        }
+    }
+};
+
+// Runs `tick(now_is_epoch)` under `mu` whenever the socket is readable, at least every
+// 50 ms, until `stop` is set: the event loop both endpoints share.
+template <class Tick>
+void event_loop(int fd, int epoch_ms, std::mutex& mu, const bool& stop, Tick&& tick) {
+    using clk = std::chrono::steady_clock;
+    const auto epoch = std::chrono::milliseconds(std::max(1, epoch_ms));
+    auto next = clk::now() + epoch;
+    for (;;) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            if (stop) return;
+        }
+        const auto now = clk::now();
+        int timeout = now >= next ? 0 : (int)std::chrono::duration_cast<std::chrono::milliseconds>(next - now).count() + 1;
+        pollfd pfd{fd, POLLIN, 0};
+        poll(&pfd, 1, std::min(timeout, 50));
+        std::lock_guard<std::mutex> lk(mu);
+        bool is_epoch = clk::now() >= next;
+        if (is_epoch) next = clk::now() + epoch;
+        tick(is_epoch);
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// LSP client (lsp/client_api.go: NewClient, Read, Write, Close)
+
+class Client {
+   public:
+    explicit Client(const Params& p) : p_(p), udp_(false) {}
+    ~Client() { stop(); }
+
+    // Blocks until the server acknowledges the connection (or EpochLimit epochs pass).
+    bool connect(const std::string& hostport) {
+        if (!udp_.dial(hostport)) return false;
+        udp_.write(lsp_marshal(LspMsg{MsgConnect, 0, 0, false, {}}), udp_.peer());
+        thread_ = std::thread([this] { event_loop(udp_.fd(), p_.epoch_ms, mu_, stop_, [this](bool e) { tick(e); }); });
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [this] { return conn_ || failed_; });
+        return conn_ != nullptr;
+    }
+
+    // Next in-order payload; false once the connection is lost and nothing is queued.
+    bool read(std::string& out) {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [this] { return !reads_.empty() || conn_->lost(); });
+        if (reads_.empty()) return false;
+        out = std::move(reads_.front());
+        reads_.pop_front();
+        return true;
+    }
+
+    bool write(const std::string& payload) {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (conn_->lost()) return false;
+        conn_->write(payload);
+        return true;
+    }
+
+    // Waits until every written message is acknowledged (or the connection is lost).
+    void close() {
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [this] { return conn_->lost() || conn_->flushed(); });
+        }
+        stop();
+    }
+
+   private:
+    Params p_;
+    Udp udp_;
+    std::thread thread_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    bool stop_ = false, failed_ = false;
+    int connect_silent_ = 0;
+    std::unique_ptr<Conn> conn_;
+    std::deque<std::string> reads_;
+
+    void stop() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        if (thread_.joinable()) thread_.join();
+    }
+
+    void tick(bool is_epoch) {  // mu_ held
+        std::string raw;
+        Addr from;
+        while (udp_.read(raw, from)) {
+            if (from != udp_.peer()) continue;
+            LspMsg m;
+            if (!lsp_unmarshal(raw, m)) continue;
+            if (!conn_) {
+                if (m.type == MsgAck && m.seq == 0 && m.conn > 0) {
+                    conn_ = std::make_unique<Conn>(m.conn, p_, [this](const LspMsg& x) {
+                        udp_.write(lsp_marshal(x), udp_.peer());
+                    });
+                    cv_.notify_all();
+                }
+                continue;
+            }
+            if (m.conn != conn_->id()) continue;
+            conn_->on_message(m, reads_);
+            cv_.notify_all();  // delivered data, or acks that may flush a close()
+        }
+        if (!is_epoch) return;
+        if (!conn_) {
+            if (++connect_silent_ >= std::max(1, p_.epoch_limit)) {
+                failed_ = true;
+                cv_.notify_all();
+            } else {
+                udp_.write(lsp_marshal(LspMsg{MsgConnect, 0, 0, false, {}}), udp_.peer());
+            }
+            return;
+        }
+        if (conn_->on_epoch()) cv_.notify_all();
+    }
+};
+
+// ---------------------------------------------------------------------------------
+// LSP server (lsp/server_api.go: NewServer, Read, Write, CloseConn, Close)
+
+class Server {
+   public:
+    struct Event {
+        long long conn = 0;
+        bool lost = false;  // the connection was lost (or closed); no payload
+        std::string payload;
+    };
+
+    explicit Server(const Params& p) : p_(p), udp_(true) {}
+    ~Server() { stop(); }
+
+    bool listen(int port) {
+        if (!udp_.listen(port)) return false;
+        thread_ = std::thread([this] { event_loop(udp_.fd(), p_.epoch_ms, mu_, stop_, [this](bool e) { tick(e); }); });
+        return true;
+    }
+    int port() const { return udp_.port(); }
+
+    // Next payload from any client, or the loss of a connection.
+    Event read() {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [this] { return !events_.empty(); });
+        Event e = std::move(events_.front());
+        events_.pop_front();
+        return e;
+    }
+
+    bool write(long long conn, const std::string& payload) {
+        std::lock_guard<std::mutex> lk(mu_);
+        auto it = conns_.find(conn);
+        if (it == conns_.end() || it->second->lost() || it->second->closing) return false;
+        it->second->write(payload);
+        return true;
+    }
+
+    // Non-blocking: pending messages to the client are still flushed, then it is dropped.
+    void close_conn(long long conn) {
+        std::lock_guard<std::mutex> lk(mu_);
+        auto it = conns_.find(conn);
+        if (it != conns_.end()) it->second->closing = true;
+    }
+
+   private:
+    Params p_;
+    Udp udp_;
+    std::thread thread_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    bool stop_ = false;
+    long long next_id_ = 1;
+    std::map<Addr, long long> id_of_;
+    std::map<long long, Addr> addr_of_;
+    std::map<long long, std::unique_ptr<Conn>> conns_;
+    std::deque<Event> events_;
+
+    void stop() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        if (thread_.joinable()) thread_.join();
+    }
+
+    void drop(long long id, bool notify) {  // mu_ held
+        auto a = addr_of_.find(id);
+        if (a != addr_of_.end()) {
+            id_of_.erase(a->second);
+            addr_of_.erase(a);
+        }
+        conns_.erase(id);
+        if (notify) {
+            events_.push_back(Event{id, true, {}});
+            cv_.notify_all();
+        }
+    }
+
+    void tick(bool is_epoch) {  // mu_ held
+        std::string raw;
+        Addr from;
+        std::deque<std::string> got;
+        while (udp_.read(raw, from)) {
+            LspMsg m;
+            if (!lsp_unmarshal(raw, m)) continue;
+            if (m.type == MsgConnect) {
+                // a repeated Connect from a known address is answered with its ID (p1.pdf p.6)
+                auto it = id_of_.find(from);
+                long long id;
+                if (it == id_of_.end()) {
+                    id = next_id_++;
+                    id_of_[from] = id;
+                    addr_of_[id] = from;
+                    conns_[id] = std::make_unique<Conn>(id, p_, [this, from](const LspMsg& x) {
+                        udp_.write(lsp_marshal(x), from);
+                    });
+                } else {
+                    id = it->second;
+                    conns_[id]->heard();
+                }
+                udp_.write(lsp_marshal(LspMsg{MsgAck, id, 0, false, {}}), from);
+                continue;
+            }
+            auto c = conns_.find(m.conn);
+            if (c == conns_.end() || addr_of_[m.conn] != from) continue;
+            got.clear();
+            c->second->on_message(m, got);
+            for (auto& p : got) events_.push_back(Event{m.conn, false, std::move(p)});
+            if (!got.empty()) cv_.notify_all();
+        }
+        if (is_epoch) {
+            for (auto& [id, c] : conns_) c->on_epoch();
+        }
+        std::vector<std::pair<long long, bool>> gone;  // lost ones notify; closed ones too
+        for (auto& [id, c] : conns_) {
+            if (c->lost()) gone.emplace_back(id, true);
+            else if (c->closing && c->flushed()) gone.emplace_back(id, true);
+        }
+        for (auto& [id, notify] : gone) drop(id, notify);
+    }
+};
+
+}  // namespace lspn

@@ -7,16 +7,9 @@
 // the Result }, and exit when the server is lost.  Go is absent here and on the GPU box,
 // so this is that program in C++ (the reference is compiled code): the min-hash loop
 // is ONE gpuhash_min call into the gfx950 engine (include/gpuhash.h), and the rest is
-// the reference's own protocol:
-//   * bitcoin.Message JSON (bitcoin/message.go:16-47) as Go's encoding/json reads and
-//     writes it;
-//   * an LSP client (lsp/client_api.go:6-30, the protocol of p1.pdf pp.2-7: Connect/Ack
-//     handshake, per-direction sequence numbers, sliding window, in-order delivery,
-//     epochs with resends and heartbeats, loss after EpochLimit silent epochs), in a
-//     background thread so heartbeats continue while a long gpuhash_min blocks;
-//   * lspnet's client-role drop injection (lspnet/staff.go:14-58) from the environment
-//     (LSPNET_CLIENT_READ_DROP / LSPNET_CLIENT_WRITE_DROP, percent), as the Python
-//     programs take it, for BASELINE config 5.
+// the reference's own protocol (lsp_native.h): bitcoin.Message JSON as Go reads and
+// writes it, an LSP client whose background thread keeps heartbeating while a long
+// gpuhash_min blocks, and lspnet's client-role drop injection for BASELINE config 5.
 // It interoperates with the Python server and client (bitcoin-miner_amd/bitcoin/).
 //
 //   gpuhash_miner host:port         (GPUHASH_DEVICES=0,1 narrows the devices;
@@ -27,34 +20,19 @@
 // GPUHASH_ETOOLONG are deterministic, so the job is logged and skipped; any other engine
 // error, or a result whose hash the host re-computation disagrees with, ends the miner
 // so the server requeues its job.  stdout is never written (the graders read it).
-#include <arpa/inet.h>
-#include <netdb.h>
-#include <poll.h>
-#include <sys/socket.h>
-#include <unistd.h>
-
-#include <chrono>
-#include <condition_variable>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
-#include <cstring>
-#include <deque>
-#include <map>
-#include <memory>
-#include <mutex>
-#include <random>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "gpuhash.h"
+#include "lsp_native.h"
 
 namespace {
 
-constexpr uint64_t kU64Max = ~0ull;
-constexpr size_t kMaxDatagram = 2000;  // the reference reads into 2000-byte buffers (lspnet/conn.go:35)
+using lspn::BtcMsg;
 
 void logf(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 void logf(const char* fmt, ...) {
@@ -66,522 +44,12 @@ void logf(const char* fmt, ...) {
     va_end(ap);
 }
 
-// ---------------------------------------------------------------------------------
-// JSON: the flat objects of lsp.Message and bitcoin.Message, read the way Go's
-// encoding/json reads them into those structs.
-
-struct JVal {
-    enum Kind { Null, Bool, Num, Str } kind = Null;
-    std::string text;  // Str: the decoded UTF-8 bytes; Num: the literal
-    bool b = false;
-};
-
-void put_utf8(std::string& out, uint32_t cp) {
-    if (cp < 0x80) {
-        out += (char)cp;
-    } else if (cp < 0x800) {
-        out += (char)(0xC0 | (cp >> 6));
-        out += (char)(0x80 | (cp & 0x3F));
-    } else if (cp < 0x10000) {
-        out += (char)(0xE0 | (cp >> 12));
-        out += (char)(0x80 | ((cp >> 6) & 0x3F));
-        out += (char)(0x80 | (cp & 0x3F));
-    } else {
-        out += (char)(0xF0 | (cp >> 18));
-        out += (char)(0x80 | ((cp >> 12) & 0x3F));
-        out += (char)(0x80 | ((cp >> 6) & 0x3F));
-        out += (char)(0x80 | (cp & 0x3F));
-    }
-}
-
-class JsonReader {
-   public:
-    explicit JsonReader(const std::string& s) : s_(s) {}
-
-    // A single JSON object whose values are scalars; false if malformed.
-    bool object(std::map<std::string, JVal>& out) {
-        ws();
-        if (!eat('{')) return false;
-        ws();
-        if (eat('}')) return end();
-        for (;;) {
-            ws();
-            std::string key;
-            if (!string(key)) return false;
-            ws();
-            if (!eat(':')) return false;
-            ws();
-            JVal v;
-            if (!value(v)) return false;
-            out[key] = v;  // Go keeps the last duplicate too
-            ws();
-            if (eat(',')) continue;
-            if (eat('}')) return end();
-            return false;
-        }
-    }
-
-   private:
-    const std::string& s_;
-    size_t i_ = 0;
-
-    void ws() {
-        while (i_ < s_.size() && (s_[i_] == ' ' || s_[i_] == '\t' || s_[i_] == '\n' || s_[i_] == '\r')) i_++;
-    }
-    bool eat(char c) {
-        if (i_ < s_.size() && s_[i_] == c) { i_++; return true; }
-        return false;
-    }
-    bool end() { ws(); return i_ == s_.size(); }
-    bool lit(const char* w) {
-        size_t n = std::strlen(w);
-        if (s_.compare(i_, n, w) != 0) return false;
-        i_ += n;
-        return true;
-    }
-    int hex4() {
-        if (i_ + 4 > s_.size()) return -1;
-        int v = 0;
-        for (int k = 0; k < 4; k++) {
-            char c = s_[i_ + (size_t)k];
-            int d = (c >= '0' && c <= '9') ? c - '0' : (c >= 'a' && c <= 'f') ? c - 'a' + 10
-                    : (c >= 'A' && c <= 'F') ? c - 'A' + 10 : -1;
-            if (d < 0) return -1;
-            v = v * 16 + d;
-        }
-        i_ += 4;
-        return v;
-    }
-    // JSON string -> UTF-8 bytes; lone or broken surrogates become U+FFFD (Go's rule)
-    bool string(std::string& out) {
-        if (!eat('"')) return false;
-        while (i_ < s_.size()) {
-            unsigned char c = (unsigned char)s_[i_++];
-            if (c == '"') return true;
-            if (c < 0x20) return false;
-            if (c != '\\') { out += (char)c; continue; }
-            if (i_ >= s_.size()) return false;
-            char e = s_[i_++];
-            switch (e) {
-                case '"': out += '"'; break;
-                case '\\': out += '\\'; break;
-                case '/': out += '/'; break;
-                case 'b': out += '\b'; break;
-                case 'f': out += '\f'; break;
-                case 'n': out += '\n'; break;
-                case 'r': out += '\r'; break;
-                case 't': out += '\t'; break;
-                case 'u': {
-                    int cp = hex4();
-                    if (cp < 0) return false;
-                    if (cp >= 0xD800 && cp < 0xDC00) {  // high surrogate: needs a low one
-                        size_t save = i_;
-                        if (lit("\\u")) {
-                            int lo = hex4();
-                            if (lo >= 0xDC00 && lo < 0xE000) {
-                                put_utf8(out, 0x10000u + (((uint32_t)cp - 0xD800u) << 10) + ((uint32_t)lo - 0xDC00u));
-                                break;
-                            }
-                        }
-                        i_ = save;
-                        put_utf8(out, 0xFFFD);
-                    } else if (cp >= 0xDC00 && cp < 0xE000) {
-                        put_utf8(out, 0xFFFD);
-                    } else {
-                        put_utf8(out, (uint32_t)cp);
-                    }
-                    break;
-                }
-                default: return false;
-            }
-        }
-        return false;
-    }
-    bool value(JVal& v) {
-        if (i_ >= s_.size()) return false;
-        char c = s_[i_];
-        if (c == '"') { v.kind = JVal::Str; return string(v.text); }
-        if (lit("null")) { v.kind = JVal::Null; return true; }
-        if (lit("true")) { v.kind = JVal::Bool; v.b = true; return true; }
-        if (lit("false")) { v.kind = JVal::Bool; v.b = false; return true; }
-        if (c == '-' || (c >= '0' && c <= '9')) {
-            size_t b = i_;
-            if (c == '-') i_++;
-            while (i_ < s_.size() && std::strchr("0123456789.eE+-", s_[i_])) i_++;
-            v.kind = JVal::Num;
-            v.text = s_.substr(b, i_ - b);
-            return true;
-        }
-        return false;  // nested objects/arrays never appear in these messages
-    }
-};
-
-// A uint64 struct field as Go's json.Unmarshal fills it: a plain non-negative integer
-// literal <= 2^64-1; null leaves the zero value.  Anything else fails the message.
-bool get_u64(const std::map<std::string, JVal>& o, const char* k, uint64_t& out) {
-    out = 0;
-    auto it = o.find(k);
-    if (it == o.end() || it->second.kind == JVal::Null) return true;
-    if (it->second.kind != JVal::Num) return false;
-    const std::string& t = it->second.text;
-    if (t.empty() || t.size() > 20) return false;
-    unsigned __int128 v = 0;
-    for (char c : t) {
-        if (c < '0' || c > '9') return false;
-        v = v * 10 + (unsigned)(c - '0');
-    }
-    if (t.size() > 1 && t[0] == '0') return false;  // not a JSON number
-    if (v > (unsigned __int128)kU64Max) return false;
-    out = (uint64_t)v;
-    return true;
-}
-
-bool get_int(const std::map<std::string, JVal>& o, const char* k, long long& out) {
-    out = 0;
-    auto it = o.find(k);
-    if (it == o.end() || it->second.kind == JVal::Null) return true;
-    if (it->second.kind != JVal::Num) return false;
-    const std::string& t = it->second.text;
-    size_t p = t[0] == '-' ? 1 : 0;
-    if (p >= t.size() || t.size() - p > 18) return false;
-    long long v = 0;
-    for (size_t i = p; i < t.size(); i++) {
-        if (t[i] < '0' || t[i] > '9') return false;
-        v = v * 10 + (t[i] - '0');
-    }
-    out = p ? -v : v;
-    return true;
-}
-
-// ---------------------------------------------------------------------------------
-// base64 (Go's StdEncoding, padded): lsp.Message.Payload is a []byte.
-
-const char kB64[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
-
-std::string b64encode(const std::string& in) {
-    std::string out;
-    size_t i = 0;
-    for (; i + 3 <= in.size(); i += 3) {
-        uint32_t v = ((uint32_t)(uint8_t)in[i] << 16) | ((uint32_t)(uint8_t)in[i + 1] << 8) | (uint8_t)in[i + 2];
-        out += kB64[v >> 18]; out += kB64[(v >> 12) & 63]; out += kB64[(v >> 6) & 63]; out += kB64[v & 63];
-    }
-    if (in.size() - i == 1) {
-        uint32_t v = (uint32_t)(uint8_t)in[i] << 16;
-        out += kB64[v >> 18]; out += kB64[(v >> 12) & 63]; out += "==";
-    } else if (in.size() - i == 2) {
-        uint32_t v = ((uint32_t)(uint8_t)in[i] << 16) | ((uint32_t)(uint8_t)in[i + 1] << 8);
-        out += kB64[v >> 18]; out += kB64[(v >> 12) & 63]; out += kB64[(v >> 6) & 63]; out += '=';
-    }
-    return out;
-}
-
-bool b64decode(const std::string& in, std::string& out) {
-    if (in.size() % 4) return false;
-    out.clear();
-    for (size_t i = 0; i < in.size(); i += 4) {
-        int v[4];
-        int pad = 0;
-        for (int k = 0; k < 4; k++) {
-            char c = in[i + (size_t)k];
-            const char* p = c ? std::strchr(kB64, c) : nullptr;
-            if (c == '=' && i + 4 == in.size() && k >= 2) { v[k] = 0; pad++; continue; }
-            if (!p || pad) return false;
-            v[k] = (int)(p - kB64);
-        }
-        uint32_t x = ((uint32_t)v[0] << 18) | ((uint32_t)v[1] << 12) | ((uint32_t)v[2] << 6) | (uint32_t)v[3];
-        out += (char)(x >> 16);
-        if (pad < 2) out += (char)((x >> 8) & 0xFF);
-        if (pad < 1) out += (char)(x & 0xFF);
-    }
-    return true;
-}
-
-// ---------------------------------------------------------------------------------
-// LSP wire messages (lsp/message.go:8-22), marshalled as Go does.
-
-enum LspType { MsgConnect = 0, MsgData = 1, MsgAck = 2 };
-
-struct LspMsg {
-    long long type = 0, conn = 0, seq = 0;
-    bool has_payload = false;
-    std::string payload;
-};
-
-std::string lsp_marshal(const LspMsg& m) {
-    std::string s = "{\"Type\":" + std::to_string(m.type) + ",\"ConnID\":" + std::to_string(m.conn) +
-                    ",\"SeqNum\":" + std::to_string(m.seq) + ",\"Payload\":";
-    s += m.has_payload ? "\"" + b64encode(m.payload) + "\"" : std::string("null");
-    return s + "}";
-}
-
-bool lsp_unmarshal(const std::string& raw, LspMsg& m) {
-    std::map<std::string, JVal> o;
-    if (!JsonReader(raw).object(o)) return false;
-    if (!get_int(o, "Type", m.type) || !get_int(o, "ConnID", m.conn) || !get_int(o, "SeqNum", m.seq)) return false;
-    auto it = o.find("Payload");
-    m.has_payload = it != o.end() && it->second.kind == JVal::Str;
-    if (it != o.end() && it->second.kind != JVal::Str && it->second.kind != JVal::Null) return false;
-    if (m.has_payload && !b64decode(it->second.text, m.payload)) return false;
-    return true;
-}
-
-// ---------------------------------------------------------------------------------
-// The client role of lspnet: one UDP socket to the server, with drop injection.
-
-int env_int(const char* name, int dflt) {
-    const char* e = std::getenv(name);
-    return e && *e ? std::atoi(e) : dflt;
-}
-
-struct Params {  // lsp/params.go:8-35, with the env overrides of bitcoin.params_from_env
-    int epoch_limit = env_int("LSP_EPOCH_LIMIT", 5);
-    int epoch_ms = env_int("LSP_EPOCH_MILLIS", 2000);
-    int window = env_int("LSP_WINDOW_SIZE", 1);
-};
-
-class Udp {
-   public:
-    bool dial(const std::string& hostport) {
-        size_t c = hostport.rfind(':');
-        if (c == std::string::npos) return false;
-        std::string host = hostport.substr(0, c), port = hostport.substr(c + 1);
-        if (host.empty()) host = "127.0.0.1";
-        addrinfo hints{}, *res = nullptr;
-        hints.ai_family = AF_INET;
-        hints.ai_socktype = SOCK_DGRAM;
-        if (getaddrinfo(host.c_str(), port.c_str(), &hints, &res) != 0 || !res) return false;
-        std::memcpy(&peer_, res->ai_addr, sizeof peer_);
-        freeaddrinfo(res);
-        fd_ = socket(AF_INET, SOCK_DGRAM, 0);
-        return fd_ >= 0;
-    }
-    ~Udp() {
-        if (fd_ >= 0) close(fd_);
-    }
-    int fd() const { return fd_; }
-    void write(const std::string& data) {
-        if (drop(wdrop_)) return;
-        sendto(fd_, data.data(), data.size(), 0, reinterpret_cast<const sockaddr*>(&peer_), sizeof peer_);
-    }
-    // one datagram from the server; false if none is ready or the injector dropped it
-    bool read(std::string& out) {
-        char buf[kMaxDatagram];
-        sockaddr_in from{};
-        socklen_t fl = sizeof from;
-        ssize_t n = recvfrom(fd_, buf, sizeof buf, MSG_DONTWAIT, reinterpret_cast<sockaddr*>(&from), &fl);
-        if (n < 0) return false;
-        if (from.sin_addr.s_addr != peer_.sin_addr.s_addr || from.sin_port != peer_.sin_port) return false;
-        if (drop(rdrop_)) return false;
-        out.assign(buf, (size_t)n);
-        return true;
-    }
-   private:
-    int fd_ = -1;
-    sockaddr_in peer_{};
-    int rdrop_ = env_int("LSPNET_CLIENT_READ_DROP", 0), wdrop_ = env_int("LSPNET_CLIENT_WRITE_DROP", 0);
-    std::mt19937 rng_{std::random_device{}()};
-    bool drop(int pct) { return pct > 0 && (int)(rng_() % 100u) < pct; }
-};
-
-// ---------------------------------------------------------------------------------
-// LSP client (lsp/client_api.go: NewClient, Read, Write, Close), protocol per p1.pdf
-// pp.2-7; the same state machine as bitcoin-miner_amd/lsp/endpoint.py.
-
-class LspClient {
-   public:
-    explicit LspClient(const Params& p) : p_(p) {}
-    ~LspClient() { stop(); }
-
-    // Blocks until the server acknowledges the connection (or EpochLimit epochs pass).
-    bool connect(const std::string& hostport) {
-        if (!udp_.dial(hostport)) return false;
-        send(LspMsg{MsgConnect, 0, 0, false, {}});
-        thread_ = std::thread([this] { loop(); });
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [this] { return conn_id_ > 0 || lost_; });
-        return conn_id_ > 0 && !lost_;
-    }
-
-    // Next in-order payload; false once the connection is lost and nothing is queued.
-    bool read(std::string& out) {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [this] { return !reads_.empty() || lost_; });
-        if (reads_.empty()) return false;
-        out = std::move(reads_.front());
-        reads_.pop_front();
-        return true;
-    }
-
-    bool write(const std::string& payload) {
-        std::lock_guard<std::mutex> lk(mu_);
-        if (lost_) return false;
-        pending_.emplace_back(next_seq_++, payload);
-        pump();
-        return true;
-    }
-
-    // Waits until every written message is acknowledged (or the connection is lost).
-    void close() {
-        {
-            std::unique_lock<std::mutex> lk(mu_);
-            cv_.wait(lk, [this] { return lost_ || (pending_.empty() && unacked_.empty()); });
-        }
-        stop();
-    }
-
-   private:
-    Params p_;
-    Udp udp_;
-    std::thread thread_;
-    std::mutex mu_;
-    std::condition_variable cv_;
-    bool stop_ = false, lost_ = false, got_data_ = false;
-    long long conn_id_ = 0;
-    int silent_ = 0;
-    long long next_seq_ = 1, expected_ = 1;
-    std::deque<std::pair<long long, std::string>> pending_;  // not yet inside the window
-    std::map<long long, std::string> unacked_;               // sent, not acknowledged
-    std::map<long long, std::string> rbuf_;                  // received out of order
-    std::deque<long long> recent_;                           // last w distinct received seqs
-    std::deque<std::string> reads_;
-
-    void stop() {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            stop_ = true;
-        }
-        if (thread_.joinable()) thread_.join();
-    }
-
-    void send(const LspMsg& m) { udp_.write(lsp_marshal(m)); }
-
-    long long window_base() const {
-        if (!unacked_.empty()) return unacked_.begin()->first;
-        if (!pending_.empty()) return pending_.front().first;
-        return next_seq_;
-    }
-
-    void pump() {  // mu_ held
-        const long long base = window_base();
-        while (!pending_.empty() && pending_.front().first < base + std::max(1, p_.window)) {
-            auto [seq, payload] = std::move(pending_.front());
-            pending_.pop_front();
-            send(LspMsg{MsgData, conn_id_, seq, true, payload});
-            unacked_.emplace(seq, std::move(payload));
-        }
-    }
-
-    void on_datagram(const std::string& raw) {  // mu_ held
-        LspMsg m;
-        if (!lsp_unmarshal(raw, m)) return;
-        if (conn_id_ == 0) {
-            if (m.type == MsgAck && m.seq == 0 && m.conn > 0) {
-                conn_id_ = m.conn;
-                silent_ = 0;
-                cv_.notify_all();
-            }
-            return;
-        }
-        if (m.conn != conn_id_) return;
-        silent_ = 0;
-        if (m.type == MsgAck) {
-            if (unacked_.erase(m.seq)) {
-                pump();
-                cv_.notify_all();
-            }
-            return;
-        }
-        if (m.type != MsgData) return;
-        send(LspMsg{MsgAck, conn_id_, m.seq, false, {}});
-        const int w = std::max(1, p_.window);
-        if (m.seq >= expected_ && m.seq < expected_ + w && !rbuf_.count(m.seq)) {
-            rbuf_.emplace(m.seq, m.payload);
-            recent_.push_back(m.seq);
-            if ((int)recent_.size() > w) recent_.pop_front();
-            got_data_ = true;
-            for (auto it = rbuf_.find(expected_); it != rbuf_.end(); it = rbuf_.find(expected_)) {
-                reads_.push_back(std::move(it->second));
-                rbuf_.erase(it);
-                expected_++;
-            }
-            cv_.notify_all();
-        }
-    }
-
-    void on_epoch() {  // mu_ held; p1.pdf p.6
-        if (lost_) return;
-        if (++silent_ >= std::max(1, p_.epoch_limit)) {
-            lost_ = true;
-            cv_.notify_all();
-            return;
-        }
-        if (conn_id_ == 0) {
-            send(LspMsg{MsgConnect, 0, 0, false, {}});
-            return;
-        }
-        if (!got_data_) send(LspMsg{MsgAck, conn_id_, 0, false, {}});
-        for (auto& [seq, payload] : unacked_) send(LspMsg{MsgData, conn_id_, seq, true, payload});
-        for (long long seq : recent_) send(LspMsg{MsgAck, conn_id_, seq, false, {}});
-    }
-
-    void loop() {
-        using clk = std::chrono::steady_clock;
-        const auto epoch = std::chrono::milliseconds(std::max(1, p_.epoch_ms));
-        auto next = clk::now() + epoch;
-        for (;;) {
-            {
-                std::lock_guard<std::mutex> lk(mu_);
-                if (stop_) return;
-            }
-            const auto now = clk::now();
-            int timeout = now >= next ? 0 : (int)std::chrono::duration_cast<std::chrono::milliseconds>(next - now).count() + 1;
-            // wake at least every 50 ms so stop() is prompt
-            pollfd pfd{udp_.fd(), POLLIN, 0};
-            poll(&pfd, 1, std::min(timeout, 50));
-            std::lock_guard<std::mutex> lk(mu_);
-            std::string raw;
-            while (udp_.read(raw)) on_datagram(raw);
-            if (clk::now() >= next) {
-                next = clk::now() + epoch;
-                on_epoch();
-            }
-        }
-    }
-};
-
-// ---------------------------------------------------------------------------------
-// bitcoin.Message (bitcoin/message.go:8-21)
-
-enum BtcType { Join = 0, Request = 1, Result = 2 };
-
-struct BtcMsg {
-    long long type = 0;
-    std::string data;
-    uint64_t lower = 0, upper = 0, hash = 0, nonce = 0;
-};
-
-bool btc_unmarshal(const std::string& raw, BtcMsg& m) {
-    std::map<std::string, JVal> o;
-    if (!JsonReader(raw).object(o)) return false;
-    if (!get_int(o, "Type", m.type)) return false;
-    auto it = o.find("Data");
-    if (it != o.end()) {
-        if (it->second.kind == JVal::Str) m.data = it->second.text;
-        else if (it->second.kind != JVal::Null) return false;
-    }
-    return get_u64(o, "Lower", m.lower) && get_u64(o, "Upper", m.upper) && get_u64(o, "Hash", m.hash) &&
-           get_u64(o, "Nonce", m.nonce);
-}
-
-// json.Marshal(bitcoin.NewJoin()) / json.Marshal(bitcoin.NewResult(h, n)): Data is empty
-std::string btc_marshal(long long type, uint64_t hash, uint64_t nonce) {
-    return "{\"Type\":" + std::to_string(type) + ",\"Data\":\"\",\"Lower\":0,\"Upper\":0,\"Hash\":" +
-           std::to_string(hash) + ",\"Nonce\":" + std::to_string(nonce) + "}";
-}
-
-std::string describe(const BtcMsg& m) {  // Message.String, message.go:49-60
-    return "[Request " + (m.data.size() > 40 ? m.data.substr(0, 40) + "..." : m.data) + " " +
-           std::to_string(m.lower) + " " + std::to_string(m.upper) + "]";
+std::string result_json(uint64_t hash, uint64_t nonce) {  // json.Marshal(bitcoin.NewResult(h, n))
+    BtcMsg r;
+    r.type = lspn::Result;
+    r.hash = hash;
+    r.nonce = nonce;
+    return lspn::btc_marshal(r);
 }
 
 std::vector<int> devices_from_env() {
@@ -607,8 +75,8 @@ int main(int argc, char** argv) {
         std::printf("Usage: ./miner <hostport>\n");
         return 0;
     }
-    Params params;
-    LspClient client(params);
+    lspn::Params params;
+    lspn::Client client(params);
     if (!client.connect(argv[1])) {
         logf("could not connect to %s", argv[1]);
         return 1;
@@ -621,15 +89,15 @@ int main(int argc, char** argv) {
         return 1;
     }
     int status = 0;
-    if (client.write(btc_marshal(Join, 0, 0))) {
+    if (client.write(lspn::btc_marshal(BtcMsg{}))) {  // json.Marshal(bitcoin.NewJoin())
         std::string payload;
         while (client.read(payload)) {
             BtcMsg m;
-            if (!btc_unmarshal(payload, m) || m.type != Request) continue;  // not a Request: ignored
+            if (!lspn::btc_unmarshal(payload, m) || m.type != lspn::Request) continue;  // not a Request: ignored
             if (m.lower > m.upper) {
                 // the spec'd loop runs zero times: the min over the empty set, which the
                 // server's lexicographic merge leaves unchanged
-                if (!client.write(btc_marshal(Result, kU64Max, kU64Max))) break;
+                if (!client.write(result_json(lspn::kU64Max, lspn::kU64Max))) break;
                 continue;
             }
             // was: for n := m.Lower; n <= m.Upper; n++ { h := bitcoin.Hash(m.Data, n) ... }
@@ -637,22 +105,23 @@ int main(int argc, char** argv) {
             rc = gpuhash_min(ctx, reinterpret_cast<const uint8_t*>(m.data.data()), m.data.size(), m.lower,
                              m.upper, &h, &n);
             if (rc == GPUHASH_EINVAL || rc == GPUHASH_ETOOLONG) {
-                logf("job %s skipped: %s", describe(m).c_str(), gpuhash_strerror(rc));
+                logf("job %s skipped: %s", lspn::btc_describe(m).c_str(), gpuhash_strerror(rc));
                 continue;  // deterministic: every miner would fail it the same way
             }
             if (rc != GPUHASH_OK) {
-                logf("job %s: %s; exiting so the server requeues it", describe(m).c_str(), gpuhash_strerror(rc));
+                logf("job %s: %s; exiting so the server requeues it", lspn::btc_describe(m).c_str(),
+                     gpuhash_strerror(rc));
                 status = 1;
                 break;
             }
             // the Go miner's optional self-check against bitcoin.Hash (hash.go:11-15)
             if (gpuhash_hash_cpu(reinterpret_cast<const uint8_t*>(m.data.data()), m.data.size(), n) != h) {
-                logf("job %s: device result (%llu, %llu) fails the host re-hash; exiting", describe(m).c_str(),
+                logf("job %s: device result (%llu, %llu) fails the host re-hash; exiting", lspn::btc_describe(m).c_str(),
                      (unsigned long long)h, (unsigned long long)n);
                 status = 1;
                 break;
             }
-            if (!client.write(btc_marshal(Result, h, n))) break;
+            if (!client.write(result_json(h, n))) break;
         }
     }
     gpuhash_close(ctx);

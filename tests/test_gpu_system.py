@@ -125,6 +125,46 @@ def test_compiled_and_python_miners_together_with_drops_and_a_kill(procs, engine
     assert "requeued" in log, log[-2000:]
 
 
+LIB = os.path.join(ROOT, "bitcoin-miner_amd", "lib")
+
+
+def start_bin(procs, argv, **extra):
+    p = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env(**extra))
+    procs.ps.append(p)
+    return p
+
+
+def test_all_compiled_config1_and_scaled_config5(procs, engine, oracle):
+    """gpuhash_server + gpuhash_miner (on the GPU) + gpuhash_client, no Python in the
+    data path: config 1's exact output, then 4 clients x 2^34 with 10% drops on every
+    role and a SIGKILLed miner."""
+    port = free_port()
+    drops = dict(LSPNET_CLIENT_READ_DROP=10, LSPNET_CLIENT_WRITE_DROP=10,
+                 LSPNET_SERVER_READ_DROP=10, LSPNET_SERVER_WRITE_DROP=10)
+    server = start_bin(procs, [os.path.join(LIB, "gpuhash_server"), str(port)],
+                       GPUHASH_JOB_SIZE=1 << 32, GPUHASH_SERVER_LOG=1, **drops)
+    time.sleep(0.5)
+    miners = [start_bin(procs, [os.path.join(LIB, "gpuhash_miner"), f"127.0.0.1:{port}"], **drops)
+              for _ in range(3)]
+    time.sleep(3.0)
+    c = start_bin(procs, [os.path.join(LIB, "gpuhash_client"), f"127.0.0.1:{port}", "bradfitz", "9999"], **drops)
+    assert c.communicate(timeout=90)[0] == "Result 1419516646206828 9898\n"
+    max_nonce = 1 << 34
+    clients = [start_bin(procs, [os.path.join(LIB, "gpuhash_client"), f"127.0.0.1:{port}", f"compiled-{i}",
+                                 str(max_nonce)], **drops) for i in range(4)]
+    time.sleep(1.0)
+    miners[0].send_signal(signal.SIGKILL)
+    for i, cl in enumerate(clients):
+        parts = cl.communicate(timeout=240)[0].split()
+        assert parts[0] == "Result", parts
+        h, n = int(parts[1]), int(parts[2])
+        msg = f"compiled-{i}".encode()
+        assert (h, n) == engine.min(msg, 0, max_nonce), i
+        assert oracle.hash(msg, n) == h
+    server.send_signal(signal.SIGTERM)
+    assert "requeued" in server.communicate(timeout=30)[1]
+
+
 def test_client_prints_disconnected_without_server(procs):
     c = procs.start([os.path.join(BIN, "client"), f"127.0.0.1:{free_port()}", "bradfitz", "9999"],
                     env=env(LSP_EPOCH_MILLIS=100, LSP_EPOCH_LIMIT=3))

@@ -29,31 +29,7 @@ P = lsp.Params(EpochLimit=20, EpochMillis=40, WindowSize=1)
 MINER_ENV = {"LSP_EPOCH_LIMIT": "20", "LSP_EPOCH_MILLIS": "40", "LSP_WINDOW_SIZE": "1"}
 
 
-_BUILDS = {}
-
-
-def build_miner(d, san=None):
-    """The miner program linked to the oracle-backed ABI shim; `san` adds host
-    sanitizers to the program's own code (the reference graders run `go test -race`;
-    SURVEY 5: sanitizers on the host code stand in for it)."""
-    key = san or "plain"
-    if key in _BUILDS:
-        return _BUILDS[key]
-    objs = []
-    for src in ("hash_oracle.c", "gpuhash_oracle_abi.c"):
-        o = str(d / f"{key}_{src}.o")
-        subprocess.check_call(["gcc", "-O2", "-c", "-I", os.path.join(ROOT, "include"),
-                               os.path.join(ROOT, "oracle", src), "-o", o])
-        objs.append(o)
-    exe = str(d / f"miner_oracle_{key.replace(',', '_')}")
-    flags = ["-O2"] if san is None else ["-O1", "-g", "-fno-omit-frame-pointer", f"-fsanitize={san}",
-                                         "-fno-sanitize-recover=all"]
-    subprocess.check_call(["g++", *flags, "-std=c++17", "-Wall", "-Wextra", "-Werror", "-I",
-                           os.path.join(ROOT, "include"),
-                           os.path.join(ROOT, "bitcoin-miner_amd", "csrc", "miner_main.cpp"), *objs,
-                           "-lpthread", "-o", exe])
-    _BUILDS[key] = exe
-    return exe
+from native_programs import SAN_MARKERS, build_miner  # noqa: E402
 
 
 @pytest.fixture(scope="module")
@@ -67,7 +43,6 @@ def miner_bin(build_dir):
 
 
 SANITIZERS = [None, "thread", "address,undefined"]
-SAN_MARKERS = ("ThreadSanitizer", "AddressSanitizer", "runtime error:", "LeakSanitizer")
 
 
 @pytest.fixture(params=SANITIZERS, ids=["plain", "tsan", "asan_ubsan"])

@@ -1,0 +1,242 @@
+"""CPU: the compiled server program (bitcoin-miner_amd/csrc/server_main.cpp -- the
+reference's server.go, spec'd in p1.pdf pp.13-15, in C++ over lsp_native.h) with
+compiled miners (built against the oracle-backed ABI shim, tests/native_programs.py),
+Python miners and Python clients over LSP/UDP: chunking and the lexicographic merge,
+balancing, a killed miner's job requeued, the requeue cap, a lost client's work dropped,
+request validation, two jobs per miner, drops on every role -- and the same runs under
+ThreadSanitizer and ASan+UBSan builds of the server.  tests/test_gpu_system.py runs the
+all-compiled system (this server, lib/gpuhash_miner on the GPU) end to end.
+"""
+import os
+import signal
+import subprocess
+import threading
+import time
+
+import pytest
+
+import bitcoin
+import lsp
+from bitcoin import client as bclient
+from bitcoin import miner as bminer
+from native_programs import Procs, build_miner, build_server
+
+P = lsp.Params(EpochLimit=20, EpochMillis=40, WindowSize=1)
+LSP_ENV = {"LSP_EPOCH_LIMIT": "20", "LSP_EPOCH_MILLIS": "40", "LSP_WINDOW_SIZE": "1"}
+
+
+def free_port():
+    import socket
+    s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture(scope="module")
+def build_dir(tmp_path_factory):
+    return tmp_path_factory.mktemp("native_server")
+
+
+@pytest.fixture(scope="module")
+def miner_bin(build_dir):
+    return build_miner(build_dir)
+
+
+@pytest.fixture
+def procs():
+    pr = Procs()
+    yield pr
+    pr.stop_all()
+    assert not pr.sanitizer_reports(), pr.sanitizer_reports()[0][-3000:]
+
+
+class System:
+    def __init__(self, procs, server_bin, miner_bin, **server_env):
+        self.procs, self.miner_bin = procs, miner_bin
+        self.port = free_port()
+        self.server = procs.start([server_bin, str(self.port)], dict(LSP_ENV, GPUHASH_SERVER_LOG=1, **server_env))
+        time.sleep(0.3)
+
+    def miner(self, **env):
+        return self.procs.start([self.miner_bin, f"127.0.0.1:{self.port}"], dict(LSP_ENV, **env))
+
+    def request(self, msg, max_nonce):
+        return bclient.request(f"127.0.0.1:{self.port}", msg, max_nonce, P)
+
+    def log(self):
+        self.server.terminate()
+        self.server.wait(10)
+        return self.server.stderr.read()
+
+
+@pytest.fixture(params=[None, "thread", "address,undefined"], ids=["plain", "tsan", "asan_ubsan"])
+def server_bin(request, build_dir):
+    return build_server(build_dir, request.param)
+
+
+@pytest.fixture
+def plain_server(build_dir):
+    return build_server(build_dir)
+
+
+def test_usage(plain_server):
+    r = subprocess.run([plain_server], capture_output=True, text=True, timeout=10)
+    assert (r.returncode, r.stdout) == (0, "Usage: ./server <port>\n")
+
+
+def test_config1_shape(procs, server_bin, miner_bin):
+    s = System(procs, server_bin, miner_bin, GPUHASH_JOB_SIZE=2500)
+    s.miner()
+    assert s.request("bradfitz", 9999) == (1419516646206828, 9898)
+    log = s.log()
+    assert "[Request bradfitz 0 9999]" in log
+
+
+def test_many_clients_compiled_and_python_miners_with_drops(procs, server_bin, miner_bin, oracle):
+    import lspnet
+    drops = dict(LSPNET_SERVER_READ_DROP=10, LSPNET_SERVER_WRITE_DROP=10)
+    s = System(procs, server_bin, miner_bin, GPUHASH_JOB_SIZE=3000, **drops)
+    for _ in range(2):
+        s.miner(LSPNET_CLIENT_READ_DROP=10, LSPNET_CLIENT_WRITE_DROP=10)
+
+    class Eng:
+        def min(self, msg, lo, hi):
+            return oracle.min(msg.encode(), lo, hi)
+
+    threading.Thread(target=bminer.run, args=(f"127.0.0.1:{s.port}", Eng(), P), daemon=True).start()
+    lspnet.SetReadDropPercent(10)
+    lspnet.SetWriteDropPercent(10)
+    results = {}
+
+    def cl(i):
+        results[i] = s.request(f"client-{i:02d}", 20000 + 777 * i)
+
+    th = [threading.Thread(target=cl, args=(i,)) for i in range(6)]
+    try:
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(120)
+    finally:
+        lspnet.ResetDropPercent()
+    for i in range(6):
+        assert results[i] == oracle.min(f"client-{i:02d}".encode(), 0, 20000 + 777 * i), i
+
+
+def test_killed_miner_job_is_requeued(procs, plain_server, miner_bin, oracle):
+    s = System(procs, plain_server, miner_bin, GPUHASH_JOB_SIZE=10 ** 7)
+    doomed = s.miner()
+    time.sleep(0.3)
+    res = {}
+    t = threading.Thread(target=lambda: res.setdefault("r", s.request("killed-miner", 2 * 10 ** 7 - 1)))
+    t.start()
+    time.sleep(1.0)  # the doomed miner is inside its first ~2 s oracle job
+    doomed.send_signal(signal.SIGKILL)
+    doomed.wait(10)
+    s.miner()
+    t.join(120)
+    assert res["r"] == oracle.min(b"killed-miner", 0, 2 * 10 ** 7 - 1, threads=8)
+    log = s.log()
+    assert "lost" in log and "requeued" in log, log
+
+
+def test_requeue_cap_disconnects_the_client(procs, plain_server, miner_bin):
+    s = System(procs, plain_server, miner_bin, GPUHASH_JOB_SIZE=1000)
+    doomed = [s.miner() for _ in range(4)]
+    time.sleep(0.3)
+    assert s.request("__gpuhash_test_ehip__", 999) is None  # every miner that takes it exits
+    for p in doomed:
+        assert p.wait(30) == 1
+    s.miner()
+    assert s.request("bradfitz", 9999) == (1419516646206828, 9898)  # and the server still serves
+    assert "abandoned" in s.log()
+
+
+def test_rejected_request_and_lost_client(procs, plain_server, miner_bin, oracle):
+    s = System(procs, plain_server, miner_bin, GPUHASH_JOB_SIZE=1000)
+    s.miner()
+    c = lsp.NewClient(f"127.0.0.1:{s.port}", P)
+    c.Write(bitcoin.marshal(bitcoin.NewRequest("x", 10, 9)))
+    with pytest.raises(lsp.LSPError):
+        c.Read()  # the server closed the connection: no job is cut
+    # a client that vanishes mid-request: its jobs stop being farmed out
+    c2 = lsp.NewClient(f"127.0.0.1:{s.port}", P)
+    c2.Write(bitcoin.marshal(bitcoin.NewRequest("gone", 0, 10 ** 7)))  # 10^4 jobs
+    time.sleep(0.3)
+    c2._loop.stop()
+    time.sleep(P.EpochLimit * P.EpochMillis / 1000 + 0.5)
+    assert s.request("bradfitz", 9999) == (1419516646206828, 9898)
+    log = s.log()
+    assert "request rejected (empty range" in log and "dropped request" in log, log
+
+
+def test_two_jobs_per_miner(procs, plain_server, miner_bin, oracle):
+    s = System(procs, plain_server, miner_bin, GPUHASH_JOB_SIZE=500, GPUHASH_MINER_DEPTH=2)
+    for _ in range(2):
+        s.miner()
+    results = {}
+    th = [threading.Thread(target=lambda i=i: results.setdefault(i, s.request(f"d2-{i}", 7000 + 333 * i)))
+          for i in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    for i in range(4):
+        assert results[i] == oracle.min(f"d2-{i}".encode(), 0, 7000 + 333 * i), i
+
+
+def test_requests_are_written_as_go_writes_them(procs, plain_server, miner_bin):
+    """The compiled server's Request payloads are byte for byte what Go's json.Marshal
+    writes (the same bytes bitcoin.marshal produces), escaped and non-ASCII Data too."""
+    s = System(procs, plain_server, miner_bin, GPUHASH_JOB_SIZE=10 ** 6)
+    m = lsp.NewClient(f"127.0.0.1:{s.port}", P)  # a bare miner: Join, then read the Request
+    m.Write(bitcoin.marshal(bitcoin.NewJoin()))
+    time.sleep(0.2)
+    c = lsp.NewClient(f"127.0.0.1:{s.port}", P)
+    data = 'héllo <&> "q" \\ \n\t\x01 ✓ \u2028'
+    c.Write(bitcoin.marshal(bitcoin.NewRequest(data, 5, 9)))
+    raw = m.Read()
+    assert raw == bitcoin.marshal(bitcoin.NewRequest(data, 5, 9)), raw
+    m.Write(bitcoin.marshal(bitcoin.NewResult(1, 5)))
+    r = bitcoin.unmarshal(c.Read())
+    assert (r.Hash, r.Nonce) == (1, 5)
+    c.Close()
+    m.Close()
+
+
+# ---- the compiled client (csrc/client_main.cpp) -------------------------------------------
+
+@pytest.fixture(scope="module")
+def client_bin(build_dir):
+    from native_programs import build_client
+    return build_client(build_dir)
+
+
+def test_client_usage_and_max_nonce_parsing(client_bin):
+    r = subprocess.run([client_bin], capture_output=True, text=True, timeout=10)
+    assert r.stdout == "Usage: ./client <hostport> <message> <maxNonce>\n"
+    for bad in ("-1", "+5", "18446744073709551616", "1e3", ""):
+        r = subprocess.run([client_bin, "127.0.0.1:1", "m", bad], capture_output=True, text=True, timeout=10)
+        assert r.stdout == f"{bad} is not a number.\n", bad
+
+
+def test_client_prints_disconnected_without_server(client_bin):
+    env = dict(os.environ, LSP_EPOCH_LIMIT="3", LSP_EPOCH_MILLIS="50")
+    r = subprocess.run([client_bin, f"127.0.0.1:{free_port()}", "bradfitz", "9999"], capture_output=True,
+                       text=True, timeout=20, env=env)
+    assert r.stdout == "Disconnected\n"
+
+
+@pytest.mark.parametrize("san", [None, "thread", "address,undefined"], ids=["plain", "tsan", "asan_ubsan"])
+def test_config1_all_compiled(procs, build_dir, miner_bin, san):
+    """Server, miner and client all compiled (the miner on the oracle-backed ABI shim
+    here; tests/test_gpu_system.py runs it on the GPU): the client prints exactly the
+    line p1.pdf p.15 grades."""
+    from native_programs import build_client
+    s = System(procs, build_server(build_dir, san), miner_bin, GPUHASH_JOB_SIZE=2000)
+    s.miner()
+    c = procs.start([build_client(build_dir, san), f"127.0.0.1:{s.port}", "bradfitz", "9999"], LSP_ENV)
+    out, err = c.communicate(timeout=60)
+    assert out == "Result 1419516646206828 9898\n", (out, err)

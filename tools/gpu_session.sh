@@ -45,6 +45,7 @@ for step in "$@"; do
         sweep) run sweep 600 python -u tools/layout_sweep.py ;;
         sys5) run sys5 900 python -u tools/system_bench.py ;;
         sys5n) run sys5n 900 python -u tools/system_bench.py --native ;;
+        sys5c) run sys5c 900 python -u tools/system_bench.py --compiled ;;
         sys5a) run sys5a 900 python -u tools/system_bench.py --adaptive
                run sys5an 900 python -u tools/system_bench.py --adaptive --native ;;
         soak) run soak 400 python -u tools/soak.py "${SOAK_SECONDS:-90}" "${SOAK_SEED:-2026}" ;;

@@ -22,7 +22,8 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "bitcoin-miner_amd", "bin")
-NATIVE_MINER = os.path.join(ROOT, "bitcoin-miner_amd", "lib", "gpuhash_miner")
+LIB = os.path.join(ROOT, "bitcoin-miner_amd", "lib")
+NATIVE_MINER = os.path.join(LIB, "gpuhash_miner")
 sys.path.insert(0, os.path.join(ROOT, "bitcoin-miner_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
@@ -48,6 +49,8 @@ def main() -> None:
                     help="the server sizes jobs per miner (GPUHASH_JOB_SECONDS=0.5) instead of fixed 2^job-bits jobs")
     ap.add_argument("--native", action="store_true",
                     help="miners are the compiled program (lib/gpuhash_miner) instead of bin/miner")
+    ap.add_argument("--compiled", action="store_true",
+                    help="server, miners and clients all compiled (lib/gpuhash_{server,miner,client})")
     args = ap.parse_args()
 
     env = dict(os.environ, LSP_EPOCH_MILLIS="500", LSP_EPOCH_LIMIT="10",
@@ -68,7 +71,11 @@ def main() -> None:
             senv["GPUHASH_JOB_SECONDS"] = "0.5"
         else:
             senv["GPUHASH_JOB_SIZE"] = str(1 << args.job_bits)
-        server = start([os.path.join(BIN, "server"), str(port)], env=senv)
+        if args.compiled:
+            args.native = True
+            server = start([os.path.join(LIB, "gpuhash_server"), str(port)], native=True, env=senv)
+        else:
+            server = start([os.path.join(BIN, "server"), str(port)], env=senv)
         time.sleep(0.5)
         ngpu = int(os.environ.get("SYSTEM_BENCH_GPUS", "0"))
         miners = []
@@ -83,8 +90,12 @@ def main() -> None:
         time.sleep(5.0)  # miners open their GPU and join
         max_nonce = (1 << args.bits)
         t0 = time.perf_counter()
-        clients = [start([os.path.join(BIN, "client"), f"127.0.0.1:{port}", f"client-{i:02d}", str(max_nonce)],
-                         env=env) for i in range(args.clients)]
+        if args.compiled:
+            clients = [start([os.path.join(LIB, "gpuhash_client"), f"127.0.0.1:{port}", f"client-{i:02d}",
+                              str(max_nonce)], native=True, env=env) for i in range(args.clients)]
+        else:
+            clients = [start([os.path.join(BIN, "client"), f"127.0.0.1:{port}", f"client-{i:02d}", str(max_nonce)],
+                             env=env) for i in range(args.clients)]
         killed = None
         if args.kill_after >= 0 and args.miners > 1:
             time.sleep(args.kill_after)
@@ -116,7 +127,7 @@ def main() -> None:
         total = args.clients * (max_nonce + 1)
         print(json.dumps({
             "workload": f"config 5: {args.clients} clients x [0, 2^{args.bits}], {args.miners} GPU miners "
-                        f"({'lib/gpuhash_miner' if args.native else 'bin/miner'}), "
+                        f"({'all compiled: gpuhash_server/miner/client' if args.compiled else 'lib/gpuhash_miner' if args.native else 'bin/miner'}), "
                         f"lspnet drop {args.drop}% on every role, "
                         f"{'per-miner jobs (~0.5 s)' if args.adaptive else f'job 2^{args.job_bits}'}, "
                         f"miner killed at {killed}s",
