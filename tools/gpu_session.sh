@@ -42,6 +42,7 @@ for step in "$@"; do
         inproc) run inproc1 300 python -u bench.py --inproc 0 --steps 5 --warmup 1
                 run inproc2 300 python -u bench.py --inproc 0,0 --steps 3 --warmup 1 ;;
         latency) run latency 120 python -u tools/latency.py ;;
+        ranks) run ranks 300 python -u tools/rank_windows.py --ranks "${RANKS:-0,1,2,3,4,5,6,7}" ;;
         sweep) run sweep 600 python -u tools/layout_sweep.py ;;
         sys5) run sys5 900 python -u tools/system_bench.py ;;
         sys5n) run sys5n 900 python -u tools/system_bench.py --native ;;
