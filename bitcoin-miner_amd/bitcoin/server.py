@@ -125,6 +125,7 @@ class Request:
     upper: int = -1       # next_lo > upper: nothing left to cut
     requeued: collections.deque = field(default_factory=collections.deque)
     inflight: int = 0
+    served: int = -1      # scheduler tick of the last job cut from it (-1: none yet)
     best: tuple | None = None
 
     def has_pending(self) -> bool:
@@ -201,7 +202,9 @@ class Scheduler:
     def next_assignment(self):
         """(miner, job, data) for the next dispatch, or None.  The miner holding the
         fewest jobs goes first (then the one served longest ago); the request with the
-        fewest jobs in flight gets it (then the oldest)."""
+        fewest jobs in flight gets it, then the one served longest ago, then the oldest:
+        a request that arrives while a long one keeps the only miner busy gets the next
+        job, instead of waiting for the long one to finish (p1.pdf p.15)."""
         free = [m for m, q in self.miners.items() if len(q) < self.depth]
         if not free:
             return None
@@ -209,8 +212,9 @@ class Scheduler:
         if not cands:
             return None
         miner = min(free, key=lambda m: (len(self.miners[m]), self._turn[m]))
-        r = min(cands, key=lambda x: (x.inflight, x.req_id))
+        r = min(cands, key=lambda x: (x.inflight, x.served, x.req_id))
         job = r.pop_job(self.size_for(miner, r))
+        r.served = next(self._tick)
         job.sent = self.clock()
         r.inflight += 1
         self.miners[miner].append(job)

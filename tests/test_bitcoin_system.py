@@ -93,6 +93,22 @@ def test_scheduler_balances_requests():
     assert s.next_assignment() is None  # no idle miners left
 
 
+def test_scheduler_does_not_starve_a_later_request():
+    """One miner, a long request in progress: a request that arrives later gets the next
+    job, and the two alternate from then on (p1.pdf p.15)."""
+    s = bserver.Scheduler(job_size=10)
+    big = s.add_request(client=100, data="a", lower=0, upper=10 ** 6)
+    s.add_miner(1)
+    m, job, _ = s.next_assignment()
+    small = s.add_request(client=101, data="b", lower=0, upper=29)
+    order = []
+    for _ in range(6):
+        s.result(m, 1, job.lower)
+        m, job, _ = s.next_assignment()
+        order.append(job.req_id)
+    assert order == [small, big, small, big, small, big]
+
+
 def test_scheduler_reassigns_lost_miner_job_first():
     s = bserver.Scheduler(job_size=10)
     s.add_request(client=100, data="a", lower=0, upper=29)

@@ -240,3 +240,21 @@ def test_config1_all_compiled(procs, build_dir, miner_bin, san):
     c = procs.start([build_client(build_dir, san), f"127.0.0.1:{s.port}", "bradfitz", "9999"], LSP_ENV)
     out, err = c.communicate(timeout=60)
     assert out == "Result 1419516646206828 9898\n", (out, err)
+
+
+def test_a_small_request_is_not_starved_by_a_large_one(procs, plain_server, miner_bin, oracle):
+    """p1.pdf p.15: the server balances miners across requests.  With one miner busy on a
+    10^4-job request, a 5-job request that arrives later is answered within a few job
+    round trips (the next job goes to the request with the fewest jobs in flight), long
+    before the large one could finish."""
+    s = System(procs, plain_server, miner_bin, GPUHASH_JOB_SIZE=2000)
+    s.miner()
+    big = lsp.NewClient(f"127.0.0.1:{s.port}", P)
+    big.Write(bitcoin.marshal(bitcoin.NewRequest("large", 0, 2 * 10 ** 7 - 1)))
+    time.sleep(0.5)
+    t0 = time.time()
+    assert s.request("bradfitz", 9999) == (1419516646206828, 9898)
+    assert time.time() - t0 < 5.0
+    big._loop.stop()  # leave without waiting: the server drops the large request
+    time.sleep(P.EpochLimit * P.EpochMillis / 1000 + 0.5)
+    assert "dropped request" in s.log()
