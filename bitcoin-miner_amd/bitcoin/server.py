@@ -125,7 +125,6 @@ class Request:
     upper: int = -1       # next_lo > upper: nothing left to cut
     requeued: collections.deque = field(default_factory=collections.deque)
     inflight: int = 0
-    served: int = -1      # scheduler tick of the last job cut from it (-1: none yet)
     best: tuple | None = None
 
     def has_pending(self) -> bool:
@@ -134,6 +133,10 @@ class Request:
     def uncut(self) -> int:
         """Nonces not yet cut into any job."""
         return max(0, self.upper - self.next_lo + 1)
+
+    def remaining(self) -> int:
+        """Nonces not yet handed to a miner: the uncut range plus requeued jobs."""
+        return self.uncut() + sum(j.upper - j.lower + 1 for j in self.requeued)
 
     def pop_job(self, size: int) -> Job:
         if self.requeued:
@@ -202,9 +205,11 @@ class Scheduler:
     def next_assignment(self):
         """(miner, job, data) for the next dispatch, or None.  The miner holding the
         fewest jobs goes first (then the one served longest ago); the request with the
-        fewest jobs in flight gets it, then the one served longest ago, then the oldest:
-        a request that arrives while a long one keeps the only miner busy gets the next
-        job, instead of waiting for the long one to finish (p1.pdf p.15)."""
+        fewest jobs in flight gets it, then the one with the least work left to hand out,
+        then the oldest.  The second key is shortest-remaining-first: a short request that
+        arrives while a long one keeps every miner busy gets the next job instead of
+        waiting for the long one to finish, and equal requests still finish one after
+        another rather than all at the end (p1.pdf p.15)."""
         free = [m for m, q in self.miners.items() if len(q) < self.depth]
         if not free:
             return None
@@ -212,9 +217,8 @@ class Scheduler:
         if not cands:
             return None
         miner = min(free, key=lambda m: (len(self.miners[m]), self._turn[m]))
-        r = min(cands, key=lambda x: (x.inflight, x.served, x.req_id))
+        r = min(cands, key=lambda x: (x.inflight, x.remaining(), x.req_id))
         job = r.pop_job(self.size_for(miner, r))
-        r.served = next(self._tick)
         job.sent = self.clock()
         r.inflight += 1
         self.miners[miner].append(job)

@@ -16,9 +16,9 @@
 //     LSP_EPOCH_LIMIT / LSP_EPOCH_MILLIS / LSP_WINDOW_SIZE, LSPNET_SERVER_{READ,WRITE}_DROP
 //
 // Scheduling: an idle miner (fewest jobs held, then longest since its last job) gets the
-// next job of the request with the fewest jobs in flight, then the one served longest ago
-// (so a request arriving while a long one holds the only miner is not starved), then the
-// oldest.  Failures: a
+// next job of the request with the fewest jobs in flight, then the least work left to hand
+// out (shortest remaining first: a short request arriving while a long one holds every
+// miner is not kept waiting, and equal requests finish in turn), then the oldest.  Failures: a
 // lost miner's jobs go back to the front of their requests' queues, at most
 // MAX_REQUEUES times per job, after which the request is abandoned and its client
 // disconnected; a lost client's requests are dropped and late results ignored.  A
@@ -76,11 +76,16 @@ struct Request {
     bool cut_all = false;  // every nonce is in some job (next_lo cannot pass 2^64-1)
     std::deque<Job> requeued;
     int inflight = 0;
-    long long served = -1;  // tick of the last job cut from it (-1: none yet)
     bool has_best = false;
     uint64_t bh = 0, bn = 0;
 
     bool has_pending() const { return !requeued.empty() || !cut_all; }
+    // nonces not yet handed to a miner (up to 2^64: hence 128 bits)
+    unsigned __int128 remaining() const {
+        unsigned __int128 n = cut_all ? 0 : (unsigned __int128)upper - next_lo + 1;
+        for (const Job& j : requeued) n += (unsigned __int128)j.hi - j.lo + 1;
+        return n;
+    }
     Job pop_job(uint64_t size) {
         if (!requeued.empty()) {
             Job j = requeued.front();
@@ -140,12 +145,13 @@ class Scheduler {
         Request* r = nullptr;
         for (auto& [id, x] : requests_) {
             if (!x.has_pending()) continue;
-            // fewest jobs in flight, then served longest ago; map order = oldest on ties
-            if (!r || x.inflight < r->inflight || (x.inflight == r->inflight && x.served < r->served)) r = &x;
+            // fewest jobs in flight, then least work left; map order = oldest on ties
+            if (!r || x.inflight < r->inflight ||
+                (x.inflight == r->inflight && x.remaining() < r->remaining()))
+                r = &x;
         }
         if (!r) return false;
         job = r->pop_job(job_size_);
-        r->served = (long long)tick_;
         r->inflight++;
         miners_[best_m].push_back(job);
         turn_[best_m] = tick_++;

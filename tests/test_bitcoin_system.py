@@ -94,8 +94,8 @@ def test_scheduler_balances_requests():
 
 
 def test_scheduler_does_not_starve_a_later_request():
-    """One miner, a long request in progress: a request that arrives later gets the next
-    job, and the two alternate from then on (p1.pdf p.15)."""
+    """One miner, a long request in progress: a short request that arrives later gets
+    the next jobs (least work left first) and finishes; then the long one resumes."""
     s = bserver.Scheduler(job_size=10)
     big = s.add_request(client=100, data="a", lower=0, upper=10 ** 6)
     s.add_miner(1)
@@ -106,7 +106,28 @@ def test_scheduler_does_not_starve_a_later_request():
         s.result(m, 1, job.lower)
         m, job, _ = s.next_assignment()
         order.append(job.req_id)
-    assert order == [small, big, small, big, small, big]
+    assert order == [small, small, small, big, big, big]
+
+
+def test_scheduler_equal_requests_finish_in_turn():
+    """Requests of equal size arriving together finish one after another (shortest
+    remaining first), not all at once at the end."""
+    s = bserver.Scheduler(job_size=10)
+    a = s.add_request(client=100, data="a", lower=0, upper=29)
+    b = s.add_request(client=101, data="b", lower=0, upper=29)
+    s.add_miner(1)
+    done, order = [], []
+    m, job, _ = s.next_assignment()
+    while True:
+        order.append(job.req_id)
+        r = s.result(m, 1, job.lower)
+        if r is not None:
+            done.append(r[0])
+        nxt = s.next_assignment()
+        if nxt is None:
+            break
+        m, job, _ = nxt
+    assert order == [a, a, a, b, b, b] and done == [100, 101]
 
 
 def test_scheduler_reassigns_lost_miner_job_first():
