@@ -100,8 +100,8 @@ def test_scheduler_accepts_full_u64_and_single_nonce():
 
 def test_requeue_cap_abandons_a_job_that_kills_every_miner():
     s = bserver.Scheduler(job_size=10, max_requeues=3)
-    rid = s.add_request(client=100, data="a", lower=0, upper=29)
-    s.add_request(client=200, data="b", lower=0, upper=9)
+    rid = s.add_request(client=100, data="a", lower=0, upper=9)
+    s.add_request(client=200, data="b", lower=0, upper=29)
     miner = 1
     s.add_miner(miner)
     m, job, _ = s.next_assignment()
