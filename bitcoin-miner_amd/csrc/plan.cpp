@@ -139,15 +139,24 @@ GroupLayout layout_for(uint64_t m, int d, uint64_t span = 0, int policy = kLayou
     // loop so block B carries loop digits only (C2 = 2: uniform schedule, no per-nonce
     // schedule work); the lanes take the digits at the end of block B-1.
     // A lane then covers R = 10^(4+q1) loop values, up to 10^8, so a narrow search fills
-    // only part of a 256-lane row: keep the classic layout (29-31 GH/s) when the expected
-    // row fill would make the uniform one (45 GH/s at full rows) slower.
+    // only part of a 256-lane row.  A wave with no lane skips the row (scan_kernel.h), but
+    // a partial row still costs more than its share of waves: measured row times, as a
+    // fraction of a full row's, for 1-4 busy waves (a wave with any lane is busy) are
+    // 0.30 / 0.58 / 0.975 / 1 when the search is that one row, and 0.33 / 0.77 / 0.98 / 1
+    // for the last row after full ones (profiles/r02_partial_rows.jsonl).  Keep the
+    // classic layout (31.7 GH/s) unless the uniform one (45.6 GH/s on full rows) is
+    // expected to be faster: lanes / (256 * row cost) >= 31.7 / 45.6 ~ 0.70.
     if (g.C2 && g.J == 1) {
         const int nb1 = d - 4 - g.q;  // digits in block B-1 and earlier
         bool fill_ok = policy != kLayoutClassic;
         if (span && policy == kLayoutAuto) {
+            static constexpr double kOneRow[5] = {0.0, 0.30, 0.58, 0.975, 1.0};
+            static constexpr double kLastRow[5] = {0.0, 0.33, 0.77, 0.98, 1.0};
             const uint64_t lanes = (span - 1) / pow10u(4 + g.q) + 1;  // lane values touched
-            const uint64_t rows = (lanes + kBlock - 1) / kBlock;
-            fill_ok = (double)lanes / (double)(rows * kBlock) >= 0.65;
+            const uint64_t full = lanes / kBlock, rem = lanes % kBlock;
+            const uint64_t busy = (rem + 63) / 64;  // busy waves of the partial row
+            const double cost = (double)full + (full ? kLastRow[busy] : kOneRow[busy]);
+            fill_ok = (double)lanes / (kBlock * cost) >= 0.70;
         }
         if (nb1 >= 3 && fill_ok) {
             g.C2 = 2;

@@ -84,7 +84,8 @@ static constexpr int kMaxLaunchDigits = 10;   // s + q <= 10  -> <= 10^10 nonces
 static constexpr int kMaxLaunchDigitsU2 = 12;
 
 // Choice between the two J = 1 straddling layouts (plan.cpp layout_for):
-//   auto     C2 = 2 (uniform two-word loop) when the search fills >= 65% of its rows
+//   auto     C2 = 2 (uniform two-word loop) when its measured partial-row cost model
+//            predicts it beats the classic layout (plan.cpp)
 //   uniform  C2 = 2 whenever block B-1 holds >= 3 digits (tuning / parity tests)
 //   classic  never C2 = 2
 enum LayoutPolicy { kLayoutAuto = 0, kLayoutUniform = 1, kLayoutClassic = 2 };

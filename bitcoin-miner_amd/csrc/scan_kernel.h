@@ -182,6 +182,17 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
     constexpr DepTable<J> kDep{};
     constexpr bool UT = C2 == 2 || (C2 == 1 && J == 0);  // uniform block-B schedule
     const uint32_t p = D.p_first + row * 256u + threadIdx.x;
+    // A wave whose 64 lanes all lie past the launch's last lane value (the tail of a
+    // partial last row) has no nonce to hash: it skips the row (up to 3.4x on one-row
+    // C2 = 2 searches, profiles/r02_partial_rows.jsonl).  Only the C2 = 2 loop has
+    // barriers (its LDS batches), so there an idle wave still walks the batches but
+    // hashes nothing.  (Rotating which wave takes which 64-lane block per workgroup, to
+    // spread the idle slots over the SIMDs, measured 1-4% slower on partial rows.)
+    const bool wave_idle =
+        __builtin_amdgcn_readfirstlane(D.p_first + row * 256u + (threadIdx.x & ~63u)) > D.p_last;
+    if constexpr (C2 != 2) {
+        if (wave_idle) return;
+    }
 
     // ---- once per row: lane words and everything that does not read W_J ----
     const uint32_t alo = ascii4(p % 10000u);
@@ -298,7 +309,7 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
                                                        K[4 * i + 2] + w[4 * i + 2], K[4 * i + 3] + w[4 * i + 3]);
             }
             __syncthreads();
-            for (uint32_t j = 0; j < nb; j++) {
+            for (uint32_t j = 0; j < (wave_idle ? 0u : nb); j++) {
                 const uint4* kr = sh_kw[j];
                 uint32_t H0, H1;
                 ut_hash(s, cv, inv0, t20, [&](int t) {

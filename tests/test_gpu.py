@@ -87,6 +87,25 @@ def test_uniform_schedule_layouts(engine, oracle, mlen, d, c2, j, request):
         assert engine.min(m, lo, hi) == oracle.min(m, lo, hi), (mlen, d, lo, hi)
 
 
+def test_idle_waves_of_partial_rows(engine, oracle, request):
+    """A row is 256 lane values (4 waves); a wave whose lanes all lie past the search's
+    last lane value skips the row (scan_kernel.h), and in the two-word uniform layout it
+    still walks the LDS batch barriers. 140 lane values: waves 0-1 full, wave 2 with 12
+    lanes, wave 3 idle, in both the two-word (C2=2) and the plain layout."""
+    import gpuhash
+    request.addfinalizer(lambda: engine.set_layout_policy(gpuhash.LAYOUT_AUTO))
+    engine.set_layout_policy(gpuhash.LAYOUT_UNIFORM)
+    # m = 58, d = 10: 5 lane digits end block B-1, 5 loop digits fill W_0/W_1 (R = 10^5)
+    m = M120[:58]
+    lo, hi = 12345 * 10 ** 5 + 678, (12345 + 139) * 10 ** 5 + 4321
+    assert engine.min(m, lo, hi) == oracle.min(m, lo, hi, threads=16)
+    assert {(r["C2"], r["J"]) for r in engine.launches()} == {(2, 1)}, engine.launches()
+    # bradfitz, d = 10: loop digits in W_4 (R = 10^3), lanes in W_2/W_3
+    lo, hi = 1234567 * 10 ** 3 + 5, (1234567 + 139) * 10 ** 3 + 998
+    assert engine.min(b"bradfitz", lo, hi) == oracle.min(b"bradfitz", lo, hi)
+    assert {(r["C2"], r["J"]) for r in engine.launches()} == {(0, 4)}, engine.launches()
+
+
 def test_layout_policies_agree(engine, request):
     """The straddling J=1 digit groups under UNIFORM, CLASSIC and AUTO: same answers
     (each is bit-exact against the oracle elsewhere; here at sizes past the oracle's)."""

@@ -111,12 +111,20 @@ def test_descriptor_replay_matches_oracle(hc, oracle, policy):
 def test_layout_policy_for_straddling_j1(hc):
     """m = 59, d = 12: digits 60..71, 4 in block 0 and 8 in block 1 (W_0 + W_1).  The
     uniform two-word loop has R = 10^8 loop values per lane, so AUTO takes it only when
-    the search fills >= 65% of its 256-lane rows; CLASSIC never, UNIFORM always."""
+    its measured partial-row cost model predicts it beats the classic layout; CLASSIC
+    never, UNIFORM always."""
     m = b"y" * 59
     lo = 10 ** 11
     narrow, wide = (lo, lo + 10 ** 9), (lo, lo + 5 * 10 ** 11)  # both stay at d = 12
     pick = lambda a, b: {(l.J, l.C2) for l in plan(hc, m, a, b)}
     assert pick(*narrow) == {(1, 1)} and pick(*wide) == {(1, 2)}
+    # lane values touched -> the uniform layout's expected rate over the classic one's
+    # (profiles/r02_partial_rows.jsonl): one row with 1-4 busy waves, then a full row
+    # plus a partial one
+    R = 10 ** 8
+    for lanes, c2 in ((45, 1), (64, 2), (100, 1), (128, 2), (160, 1), (192, 2), (215, 2),
+                      (300, 2), (330, 2), (400, 2)):
+        assert pick(lo, lo + lanes * R - 1) == {(1, c2)}, lanes
     try:
         hc.hostcheck_set_layout_policy(UNIFORM)
         assert pick(*narrow) == {(1, 2)}

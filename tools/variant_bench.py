@@ -25,7 +25,8 @@ with gpuhash.Engine([0], lib_path=sys.argv[1]) as e:
              ("j13", b"y" * 44, 10**9, 10**9 + (1 << 31)),         # plain, late loop word
              ("j2", b"", 10**9, 10**9 + (1 << 31)),                # plain, early loop word
              ("cj1", b"c" * 61, 10**9, 10**9 + (1 << 31)),         # classic straddle C2=1, J=1
-             ("u2f", b"u" * 58, 10240 * 10**7, 10240 * 10**7 + 256 * 10**7 - 1)]  # C2=2, one full row
+             ("u2f", b"u" * 58, 10240 * 10**7, 10240 * 10**7 + 256 * 10**7 - 1),  # C2=2, one full row
+             ("u2p", b"u" * 60, 10**9, (1 << 32) - 1)]  # C2=2, 430 lane values: wave 3 of row 2 idle
     for name, msg, lo, hi in cases:
         e.min(msg, lo, hi)
         best, res = 1e9, None
