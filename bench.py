@@ -325,7 +325,10 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    # dominant kernel = the variant with the most HIP-event time in the timed region
+    # dominant kernel = the variant with the most algorithmic work (nonces x blocks) in
+    # the timed region.  On a GPU of its own that is also the one with the most HIP-event
+    # time; ranks rehearsed on one shared GPU wait behind each other's launches, so their
+    # event time would pick a short launch that happened to queue.
     by = {}
     for r in recs:
         k = (r["J"], r["C2"], r["EX"])
@@ -334,7 +337,7 @@ def main() -> None:
         e["clk_ms"] += r["sclk_mhz"] * r["ms"]  # ms-weighted in-kernel shader clock
         e["n"] += 1
         e["nonces"] += r["nonces"]
-    key, dom = max(by.items(), key=lambda kv: kv[1]["ms"])
+    key, dom = max(by.items(), key=lambda kv: kv[1]["nonces"] * kv[1]["c"])
     avg_ms = dom["ms"] / dom["n"]
     ops_per_launch = dom["nonces"] / dom["n"] * OPS_PER_BLOCK * dom["c"]
     achieved_T = ops_per_launch / (avg_ms * 1e-3) / 1e12
