@@ -2,7 +2,7 @@
 # tools/gpu_session.sh STEP... -- runs GPU steps on the gpurun box, each under its own
 # time limit, logging to gpurun_out/.  A plain failure (exit 1, e.g. a failing test)
 # lets the next step run; a fault, abort, segfault, time limit or kill stops the session.
-# Steps: valu | go | test | soak | smoke | bench | bench3 | bench4 | prof4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | pmc3 | sweep | variants | partial | regret | sys5
+# Steps: valu | go | test | soak | smoke | bench | bench3 | bench4 | prof4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | pmc3 | pmc4 | sweep | variants | partial | regret | sys5
 set -u
 cd "$(dirname "$0")/.."
 OUT=gpurun_out
@@ -69,6 +69,12 @@ for step in "$@"; do
               run pmc_derived_c3 120 rocprofv3 --pmc VALUBusy VALUUtilization -d "$OUT/pmc4_c3" -o pmc --output-format csv -- $B3
               run pmc_hbm_c3 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc2_c3" -o pmc --output-format csv -- $B3
               run pmc_wr_c3 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc3_c3" -o pmc --output-format csv -- $B3 ;;
+        pmc4) B4="python3 bench.py --config 4 --steps 1 --warmup 1 --no-cpu-baseline"
+              run prof_c4 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c4" -o bench --output-format csv -- $B4
+              run pmc_valu_c4 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/pmc1_c4" -o pmc --output-format csv -- $B4
+              run pmc_derived_c4 120 rocprofv3 --pmc VALUBusy VALUUtilization -d "$OUT/pmc4_c4" -o pmc --output-format csv -- $B4
+              run pmc_hbm_c4 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc2_c4" -o pmc --output-format csv -- $B4
+              run pmc_wr_c4 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc3_c4" -o pmc --output-format csv -- $B4 ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
