@@ -7,8 +7,14 @@ SHA block), 2^32 nonces -- per GPU, i.e. gpuhash_min over the rank's shard plus 
 16-byte cross-rank merge.  Weak scaling: rank r searches [r*2^32, (r+1)*2^32).
 
   python bench.py                       # N=1, defaults finish in well under a minute
+  python bench.py --gpus N              # ONE process drives devices 0..N-1 (the north_star
+                                        # design: cost-balanced shards, a host thread +
+                                        # stream per device, 16-byte host argmin); exits
+                                        # non-zero when fewer than N devices are visible
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
       --master-port P bench.py --gpus N --steps K --warmup W
+                                        # one process per GPU (the driver's N>1 launch);
+                                        # --gpus must equal WORLD_SIZE
 
 Inputs are resident on the device before timing (the message is a kernel argument;
 the nonce space is generated in registers), so value = whole-job nonces / max-over-
@@ -197,12 +203,128 @@ def emit(out: dict) -> None:
         os.write(_JSON_FD, line)
 
 
-def main_inproc(args) -> None:
-    """All devices in ONE process: each step is one gpuhash_min over the union of the
-    per-GPU windows of ranks 0..N-1 (config 2/4: [0, N*per_gpu), weak scaling; config 3:
-    the same two windows split over N devices, strong scaling)."""
+def dominant(recs: list[dict]) -> tuple[tuple, dict]:
+    """The dominant scan variant of a list of launch records: the one with the most
+    algorithmic work (nonces x blocks).  On a GPU of its own that is also the one with the
+    most HIP-event time; ranks rehearsed on one shared GPU wait behind each other's
+    launches, so their event time would pick a short launch that happened to queue."""
+    by = {}
+    for r in recs:
+        k = (r["J"], r["C2"], r["EX"])
+        e = by.setdefault(k, {"ms": 0.0, "n": 0, "nonces": 0, "c": r["c"], "clk_ms": 0.0})
+        e["ms"] += r["ms"]
+        e["clk_ms"] += r["sclk_mhz"] * r["ms"]  # ms-weighted in-kernel shader clock
+        e["n"] += 1
+        e["nonces"] += r["nonces"]
+    return max(by.items(), key=lambda kv: kv[1]["nonces"] * kv[1]["c"])
+
+
+def roofline(config: str, recs: list[dict]) -> dict:
+    """roofline object of the bench line for the dominant kernel of `recs` (HIP-event
+    timed on the library's own stream in this run)."""
+    key, dom = dominant(recs)
+    avg_ms = dom["ms"] / dom["n"]
+    ops_per_launch = dom["nonces"] / dom["n"] * OPS_PER_BLOCK * dom["c"]
+    achieved_T = ops_per_launch / (avg_ms * 1e-3) / 1e12
+    kernel_ghs = dom["nonces"] / (dom["ms"] * 1e-3) / 1e9
+    sclk = dom["clk_ms"] / dom["ms"] if dom["ms"] > 0 else 0.0  # MHz, measured in the kernel
+    peak_at_clk = 256 * 128 * sclk * 1e6 / 1e12  # the guide's peak at the measured clock
+    pmc, prov = pmc_source(config, key)
+    insts = pmc_issued(pmc)
+    issued_per_nonce = insts * 64 / (dom["nonces"] / dom["n"]) if insts else None
+    issued_T = kernel_ghs * issued_per_nonce / 1e3 if issued_per_nonce else None
+    return {
+        "bound": "valu",
+        # algorithmic: SURVEY 8(d)'s 1,378 lane-ops per nonce-bearing block x the
+        # launch's nonces / its HIP-event time
+        "achieved": round(achieved_T, 3),
+        "peak": round(VALU_PEAK_T, 3),
+        "unit": "T int32 lane-ops/s",
+        "frac": round(achieved_T / VALU_PEAK_T, 4),
+        "frac_basis": "algorithmic ops / the guide's SIMD-32 VALU peak (2-cycle wave64 issue)"
+                      + ("; the algorithmic count charges c=2 blocks per nonce but this layout "
+                         "compresses block B-1 once per lane row, so frac exceeds 1: issued_frac "
+                         "is the hardware-bounded figure" if achieved_T > VALU_PEAK_T else ""),
+        "traffic": pmc_traffic(pmc),
+        "kernel": f"k_scan<J={key[0]},C2={key[1]},EX={key[2]},MODE=0>",
+        "avg_launch_ms": round(avg_ms, 4),
+        "nonces_per_launch": dom["nonces"] / dom["n"],
+        "ops_per_nonce": OPS_PER_BLOCK * dom["c"],
+        "kernel_GHs": round(kernel_ghs, 4),
+        # hardware-counted view: SQ_INSTS_VALU x 64 / nonce from the committed PMC
+        # pass of this build (pmc_source), times this run's kernel rate
+        "issued_lane_instr_per_nonce": round(issued_per_nonce, 1) if issued_per_nonce else None,
+        "issued_T": round(issued_T, 3) if issued_T else None,
+        "issued_frac": round(issued_T / VALU_PEAK_T, 4) if issued_T else None,
+        # SURVEY 8(d)'s 39.3 T = every instruction at 4 cycles per wave64, the cost of
+        # v_alignbit / v_add3 / v_bfi (DESIGN 4.1): where a rotate-bearing stream settles
+        "survey_peak": round(SURVEY_PEAK_T, 3),
+        "frac_vs_survey_peak": round(achieved_T / SURVEY_PEAK_T, 4),
+        "issued_frac_vs_survey_peak": round(issued_T / SURVEY_PEAK_T, 4) if issued_T else None,
+        "peak_basis": "MI355X_MICROARCH.md: 4 SIMD-32/CU, wave64 VALU issue every 2 cycles, "
+                      "256 CU at 2.4 GHz; SURVEY 8(d) 4-cycle figure as survey_peak",
+        "pmc_source": prov,
+        # shader clock over the dominant launches, from s_memtime / s_memrealtime in
+        # workgroup 0 (SURVEY 7: record the sustained sclk beside every GH/s)
+        "sclk_mhz": round(sclk, 1),
+        "peak_at_sclk": round(peak_at_clk, 3),
+        "frac_at_sclk": round(achieved_T / peak_at_clk, 4) if peak_at_clk else None,
+    }
+
+
+def per_device(recs: list[dict], steps: int) -> tuple[list[dict], int, list[dict]]:
+    """Per device (shard) of the in-process path: its launches' HIP-event time per step,
+    nonces per step and kernel rate; plus the SLOWEST device (most kernel time: it sets the
+    step time) and its launch records, whose dominant kernel is the line's roofline."""
+    by = {}
+    for r in recs:
+        e = by.setdefault(r["device"], {"recs": [], "ms": 0.0, "nonces": 0})
+        e["recs"].append(r)
+        e["ms"] += r["ms"]
+        e["nonces"] += r["nonces"]
+    slow = max(by, key=lambda d: by[d]["ms"])
+    rows = [{"device": d, "kernel_ms_per_step": round(e["ms"] / steps, 3),
+             "nonces_per_step": e["nonces"] // steps,
+             "kernel_GHs": round(e["nonces"] / (e["ms"] * 1e-3) / 1e9, 4) if e["ms"] > 0 else None}
+            for d, e in sorted(by.items())]
+    return rows, slow, by[slow]["recs"]
+
+
+def base_line(args, value: float, n: int, dt: float, workload: str, msg: bytes, parallelism: str,
+              scaling: str, **config) -> dict:
+    return {
+        "metric": METRIC, "value": round(value, 4), "unit": "GH/s", "n_gpus": n,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (the nonce space itself; fixed message)",
+        "config": {"workload": workload, "msg_len": len(msg), "parallelism": parallelism, **config},
+        "per_gpu_GHs": round(value / n, 4),
+    }
+
+
+def add_cpu_baselines(out: dict, args) -> None:
+    if not args.no_cpu_baseline and args.config == "2":
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        out["cpu_baseline_multicore"] = cpu_baseline_multicore(args.cpu_seconds / 2)
+        out["cpu_baseline_plain_c"] = cpu_baseline_plain_c(args.cpu_seconds / 4)
+
+
+def fail(msg: str) -> None:
+    print(f"bench.py: {msg}", file=sys.stderr)
+    sys.exit(2)
+
+
+def main_inproc(args, devs: list[int]) -> None:
+    """All devices in ONE process, the north_star's design: one gpuhash context over
+    devices `devs`, each step one gpuhash_min over the union of the per-GPU windows of
+    ranks 0..N-1 (config 2/4: [0, N*per_gpu), weak scaling; config 3: the same two windows
+    split over N devices, strong scaling).  Inside the call the engine cuts the range into
+    N contiguous shards of equal estimated cost (gpuhash_shard_range), runs each on its
+    device's own host thread + HIP stream, and takes the 16-byte host argmin: no
+    collective, no torch.distributed."""
+    import torch
     import gpuhash
-    devs = None if args.inproc == "all" else [int(x) for x in args.inproc.split(",")]
+    from gpuhash.dist import merge_min
     eng = gpuhash.Engine(devs)
     n = eng.ndevices
     cfg = CONFIGS[args.config]
@@ -217,83 +339,74 @@ def main_inproc(args) -> None:
     total_per_step = sum(hi - lo + 1 for lo, hi in merged)
 
     def step(recs=None):
-        from gpuhash.dist import merge_min
         parts = []
         for lo, hi in merged:
-            parts.append(eng.min(msg, lo, hi))
+            parts.append(eng.min(msg, lo, hi))  # blocking: every device's stream is synced
             if recs is not None:
                 recs.extend(eng.launches())
         return merge_min(parts)
 
+    def barrier():  # gpuhash_min returns after its streams finish; torch's are idle
+        for d in sorted(set(devs)):
+            torch.cuda.synchronize(d)
+
     for _ in range(args.warmup):
         step()
+    barrier()
     recs = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = step(recs)
+    barrier()
     dt = time.perf_counter() - t0
     value = total_per_step * args.steps / dt / 1e9
-    out = {
-        "metric": METRIC, "value": round(value, 4), "unit": "GH/s", "n_gpus": n,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
-        "higher_is_better": True, "scaling": "strong" if args.config == "3" else "weak",
-        "vs_baseline": None, "dtype": "u32", "data": "synthetic (the nonce space itself; fixed message)",
-        "config": {"workload": cfg["desc"] + " -- in-process, one gpuhash context over all devices",
-                   "msg_len": len(msg), "ranges": [list(w) for w in merged],
-                   "parallelism": f"inproc{n}", "devices": devs or "all"},
-        "per_gpu_GHs": round(value / n, 4), "result": list(res),
-        "launches_per_step": len(recs) // max(args.steps, 1),
-    }
+    scaling = "strong" if args.config == "3" else "weak"
+    out = base_line(args, value, n, dt, cfg["desc"] + (" -- in-process, one gpuhash context over all devices"
+                                                      if n > 1 else ""),
+                    msg, f"inproc{n}" if n > 1 else "single", scaling,
+                    nonces_per_step=total_per_step, ranges=[list(w) for w in merged], devices=devs)
+    out["per_device"], slow, slow_recs = per_device(recs, args.steps)
+    out["result"] = list(res)
+    out["launches_per_step"] = len(recs) // max(args.steps, 1)
+    out["roofline"] = roofline(args.config, slow_recs)
+    out["roofline"]["device"] = slow
+    if n == 1:
+        add_cpu_baselines(out, args)
     emit(out)
     eng.close()
 
 
-def main() -> None:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--config", default="2", choices=sorted(CONFIGS))
-    ap.add_argument("--inproc", default=None, metavar="DEVICES",
-                    help="one process drives these HIP devices (comma list or 'all') through "
-                         "one gpuhash context: static cost-balanced shards, one host thread + "
-                         "stream per device, 16-byte host argmin (SURVEY 8(e)); not used by "
-                         "the torchrun path")
-    args = ap.parse_args()
-    _quiet_stdout()
-    if args.inproc is not None:
-        return main_inproc(args)
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+def main_ranks(args, world: int, rank: int, local: int) -> None:
+    """One process per GPU (torch.distributed.run): rank r searches its own window(s) on
+    device LOCAL_RANK.  No collective on the data path: the ranks' 24-byte results are
+    merged on the host (a gloo all_gather over TCP, once per step), and the only other
+    traffic is the timing contract's barrier and max-over-ranks.  GPUHASH_DIST_BACKEND=nccl
+    moves those onto RCCL instead (GPUHASH_FORCE_DIST=1 runs this path at WORLD_SIZE=1)."""
     import torch
-    dist = None
-    # one process per GPU; GPUHASH_DIST_BACKEND=gloo lets several ranks share one GPU
-    # (rehearsing the N>1 path on a 1-GPU box), nccl (= RCCL) is the default
-    backend = os.environ.get("GPUHASH_DIST_BACKEND", "nccl")
-    ndev = max(torch.cuda.device_count(), 1)
-    local = local % ndev
-    # GPUHASH_FORCE_DIST=1 runs the collective path even at WORLD_SIZE=1, so a 1-GPU box
-    # exercises the RCCL init / all_gather / all_reduce calls the 8-GPU run makes
-    if world > 1 or os.environ.get("GPUHASH_FORCE_DIST") == "1":
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-
+    import torch.distributed as dist
     import gpuhash
     from gpuhash.dist import gather_results, merge_min
+    backend = os.environ.get("GPUHASH_DIST_BACKEND", "gloo")
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        fail("no visible GPU")
+    shared = os.environ.get("GPUHASH_SHARE_GPU") == "1"  # rehearsal: ranks share device 0..
+    if local >= ndev and not shared:
+        fail(f"LOCAL_RANK {local} but only {ndev} visible device(s); "
+             "set GPUHASH_SHARE_GPU=1 to rehearse several ranks on one GPU")
+    local = local % ndev
+    torch.cuda.set_device(local)
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend)
+    dev = torch.device("cuda", local)
+    coll_dev = dev if backend == "nccl" else None  # gloo moves CPU tensors
+
     eng = gpuhash.Engine([local])
     cfg = CONFIGS[args.config]
     msg, windows = cfg["msg"], cfg["windows"](rank)
     per_gpu = sum(hi - lo + 1 for lo, hi in windows)
-    dev = torch.device("cuda", local)
-    coll_dev = dev if backend == "nccl" else None  # gloo gathers CPU tensors
 
     def step(recs=None):
         parts = []
@@ -301,15 +414,11 @@ def main() -> None:
             parts.append(eng.min(msg, lo, hi))
             if recs is not None:
                 recs.extend(eng.launches())  # HIP-event time of every scan launch
-        res = merge_min(parts)
-        if dist is not None:
-            res = merge_min(gather_results(res, coll_dev))
-        return res
+        return merge_min(gather_results(merge_min(parts), coll_dev))
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
         torch.cuda.synchronize(dev)
+        dist.barrier()
 
     for _ in range(args.warmup):
         step()
@@ -320,104 +429,62 @@ def main() -> None:
         res = step(recs)
     barrier()
     dt = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev or "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-
-    # dominant kernel = the variant with the most algorithmic work (nonces x blocks) in
-    # the timed region.  On a GPU of its own that is also the one with the most HIP-event
-    # time; ranks rehearsed on one shared GPU wait behind each other's launches, so their
-    # event time would pick a short launch that happened to queue.
-    by = {}
-    for r in recs:
-        k = (r["J"], r["C2"], r["EX"])
-        e = by.setdefault(k, {"ms": 0.0, "n": 0, "nonces": 0, "c": r["c"], "clk_ms": 0.0})
-        e["ms"] += r["ms"]
-        e["clk_ms"] += r["sclk_mhz"] * r["ms"]  # ms-weighted in-kernel shader clock
-        e["n"] += 1
-        e["nonces"] += r["nonces"]
-    key, dom = max(by.items(), key=lambda kv: kv[1]["nonces"] * kv[1]["c"])
-    avg_ms = dom["ms"] / dom["n"]
-    ops_per_launch = dom["nonces"] / dom["n"] * OPS_PER_BLOCK * dom["c"]
-    achieved_T = ops_per_launch / (avg_ms * 1e-3) / 1e12
-    kernel_ghs = dom["nonces"] / (dom["ms"] * 1e-3) / 1e9
-    sclk = dom["clk_ms"] / dom["ms"] if dom["ms"] > 0 else 0.0  # MHz, measured in the kernel
-    peak_at_clk = 256 * 128 * sclk * 1e6 / 1e12  # the guide's peak at the measured clock
-    pmc, prov = pmc_source(args.config, key)
-    insts = pmc_issued(pmc)
-    issued_per_nonce = insts * 64 / (dom["nonces"] / dom["n"]) if insts else None
-    issued_T = kernel_ghs * issued_per_nonce / 1e3 if issued_per_nonce else None
-
+    t = torch.tensor([dt], dtype=torch.float64, device=coll_dev or "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    roof = roofline(args.config, recs)
     if rank == 0:
-        total = per_gpu * world * args.steps
-        value = total / dt / 1e9
-        out = {
-            "metric": METRIC,
-            "value": round(value, 4),
-            "unit": "GH/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": "synthetic (the nonce space itself; fixed message)",
-            "config": {"workload": cfg["desc"], "msg_len": len(msg), "nonces_per_gpu": per_gpu,
-                       "parallelism": f"dp{world}"},
-            "per_gpu_GHs": round(value / world, 4),
-            "result_rank0_range": list(res) if world == 1 else None,
-            "result": list(res),  # (hash, nonce) argmin over every rank's windows
-            "roofline": {
-                "bound": "valu",
-                # algorithmic: SURVEY 8(d)'s 1,378 lane-ops per nonce-bearing block x the
-                # launch's nonces / its HIP-event time
-                "achieved": round(achieved_T, 3),
-                "peak": round(VALU_PEAK_T, 3),
-                "unit": "T int32 lane-ops/s",
-                "frac": round(achieved_T / VALU_PEAK_T, 4),
-                "frac_basis": "algorithmic ops / the guide's SIMD-32 VALU peak (2-cycle wave64 issue)"
-                              + ("; the algorithmic count charges c=2 blocks per nonce but this layout "
-                                 "compresses block B-1 once per lane row, so frac exceeds 1: issued_frac "
-                                 "is the hardware-bounded figure" if achieved_T > VALU_PEAK_T else ""),
-                "traffic": pmc_traffic(pmc),
-                "kernel": f"k_scan<J={key[0]},C2={key[1]},EX={key[2]},MODE=0>",
-                "avg_launch_ms": round(avg_ms, 4),
-                "nonces_per_launch": dom["nonces"] / dom["n"],
-                "ops_per_nonce": OPS_PER_BLOCK * dom["c"],
-                "kernel_GHs": round(kernel_ghs, 4),
-                # hardware-counted view: SQ_INSTS_VALU x 64 / nonce from the committed PMC
-                # pass of this build (pmc_source), times this run's kernel rate
-                "issued_lane_instr_per_nonce": round(issued_per_nonce, 1) if issued_per_nonce else None,
-                "issued_T": round(issued_T, 3) if issued_T else None,
-                "issued_frac": round(issued_T / VALU_PEAK_T, 4) if issued_T else None,
-                # SURVEY 8(d)'s 39.3 T = every instruction at 4 cycles per wave64, the cost of
-                # v_alignbit / v_add3 / v_bfi; SHA-256 cannot avoid them, so
-                # this is where a rotate-bearing stream settles, not a hard ceiling: the
-                # few 2-cycle instructions left in the stream put issued_T slightly above it
-                "survey_peak": round(SURVEY_PEAK_T, 3),
-                "frac_vs_survey_peak": round(achieved_T / SURVEY_PEAK_T, 4),
-                "issued_frac_vs_survey_peak": round(issued_T / SURVEY_PEAK_T, 4) if issued_T else None,
-                "peak_basis": "MI355X_MICROARCH.md: 4 SIMD-32/CU, wave64 VALU issue every 2 cycles, "
-                              "256 CU at 2.4 GHz; SURVEY 8(d) 4-cycle figure as survey_peak",
-                "pmc_source": prov,
-                # shader clock over the dominant launches, from s_memtime / s_memrealtime
-                # in workgroup 0 (record the sustained sclk beside every GH/s)
-                "sclk_mhz": round(sclk, 1),
-                "peak_at_sclk": round(peak_at_clk, 3),
-                "frac_at_sclk": round(achieved_T / peak_at_clk, 4) if peak_at_clk else None,
-            },
-        }
-        if world == 1 and not args.no_cpu_baseline and args.config == "2":
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-            out["cpu_baseline_multicore"] = cpu_baseline_multicore(args.cpu_seconds / 2)
-            out["cpu_baseline_plain_c"] = cpu_baseline_plain_c(args.cpu_seconds / 4)
+        value = per_gpu * world * args.steps / dt / 1e9
+        out = base_line(args, value, world, dt, cfg["desc"], msg, f"dp{world}", "weak",
+                        nonces_per_gpu=per_gpu, processes=world, backend=backend)
+        out["result"] = list(res)  # (hash, nonce) argmin over every rank's windows
+        out["roofline"] = roof
+        if world == 1:
+            add_cpu_baselines(out, args)
         emit(out)
     eng.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    dist.destroy_process_group()
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs to drive: under torch.distributed.run it must equal WORLD_SIZE "
+                         "(one process per GPU); otherwise ONE process drives devices 0..N-1 "
+                         "through one gpuhash context")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--config", default="2", choices=sorted(CONFIGS))
+    ap.add_argument("--inproc", default=None, metavar="DEVICES",
+                    help="explicit device list for the one-process path (comma list, ordinals "
+                         "may repeat to rehearse N shards on one GPU); overrides --gpus")
+    args = ap.parse_args()
+    if args.gpus < 1:
+        fail("--gpus must be >= 1")
+    _quiet_stdout()
+    # torch before libgpuhash: both link libamdhip64, and the process must load torch's
+    # HIP runtime first, or torch later finds "No HIP GPUs are available"
+    import torch  # noqa: F401
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is not None and (int(world_env) > 1 or os.environ.get("GPUHASH_FORCE_DIST") == "1"):
+        world = int(world_env)
+        if args.inproc is not None:
+            fail("--inproc is the one-process path; do not launch it under torch.distributed.run")
+        if world != args.gpus:
+            fail(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one process per GPU")
+        return main_ranks(args, world, int(os.environ.get("RANK", "0")),
+                          int(os.environ.get("LOCAL_RANK", "0")))
+    import gpuhash
+    visible = gpuhash.device_count()
+    if args.inproc is not None:
+        devs = [int(x) for x in args.inproc.split(",")]
+    else:
+        devs = list(range(args.gpus))
+    if not devs or max(devs) >= visible or min(devs) < 0:
+        fail(f"asked for device(s) {devs} but {visible} HIP device(s) are visible")
+    return main_inproc(args, devs)
 
 
 if __name__ == "__main__":

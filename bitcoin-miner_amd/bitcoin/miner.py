@@ -57,17 +57,19 @@ def run(hostport: str, engine=None, params=None, on_client=None) -> int:
             # was: for n := m.Lower; n <= m.Upper; n++ { h := bitcoin.Hash(m.Data, n) ... }
             try:
                 h, n = engine.min(m.Data, m.Lower, m.Upper)
-            except (ValueError, TypeError) as e:
-                _log(f"job {m} skipped: {e}")
-                continue
             except Exception as e:
-                if getattr(e, "is_argument_error", False):
-                    # deterministic (EINVAL/ETOOLONG): every miner would fail it the same
-                    # way, so it is skipped rather than exiting (which would requeue it
-                    # to the next miner); the server validates requests so that its own
-                    # jobs never get here
-                    _log(f"job {m} skipped: {e}")
-                    continue
+                if isinstance(e, (ValueError, TypeError)) or getattr(e, "is_argument_error", False):
+                    # deterministic (EINVAL/ETOOLONG): no Result can be sent for this job,
+                    # and skipping it would leave it in flight forever (the server pairs
+                    # each Result with the miner's OLDEST job, so with two jobs per miner
+                    # the next Result would even answer the wrong request).  So the miner
+                    # exits like on a device error: the server sees the connection lost,
+                    # requeues the job, and its requeue cap (server.MAX_REQUEUES) ends the
+                    # request with Disconnected at the client after the job has failed a
+                    # few miners.  The in-tree servers validate requests, so their jobs
+                    # never get here.
+                    _log(f"job {m} failed: {e}; exiting so the server requeues it")
+                    return 1
                 # a device error (no device, HIP failure) propagates: the miner exits and
                 # the server requeues the job on another miner (p1.pdf p.15), at most
                 # server.MAX_REQUEUES times

@@ -382,6 +382,34 @@ static int open_impl(const int* devices, int ndevices, gpuhash_ctx** out) {
 
 int gpuhash_ndevices(const gpuhash_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
 
+int gpuhash_device_count(void) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count < 0) return 0;
+    return count;
+}
+
+int gpuhash_shard_range(size_t msg_len, uint64_t lower, uint64_t upper, int nshards,
+                        uint64_t* out_lower, uint64_t* out_upper) {
+    if (nshards < 1 || !out_lower || !out_upper || lower > upper) return GPUHASH_EINVAL;
+    if (msg_len > GPUHASH_MAX_MSG) return GPUHASH_ETOOLONG;
+    try {
+        // the same cost model and cut points as gpuhash_min's in-process shards
+        const std::vector<Shard> sh = shard_range(msg_len, lower, upper, nshards);
+        int used = 0;
+        for (int k = 0; k < nshards; k++) {
+            const Shard& s = sh[(size_t)k];
+            out_lower[k] = s.empty ? 1 : s.lo;
+            out_upper[k] = s.empty ? 0 : s.hi;
+            used += s.empty ? 0 : 1;
+        }
+        return used;
+    } catch (const std::bad_alloc&) {
+        return GPUHASH_ENOMEM;
+    } catch (...) {
+        return GPUHASH_EHIP;
+    }
+}
+
 int gpuhash_set_layout_policy(gpuhash_ctx* ctx, int policy) {
     if (!ctx || policy < GPUHASH_LAYOUT_AUTO || policy > GPUHASH_LAYOUT_CLASSIC) return GPUHASH_EINVAL;
     std::lock_guard<std::mutex> lock(ctx->mu);

@@ -16,10 +16,12 @@
 //                                    LSP_EPOCH_LIMIT / LSP_EPOCH_MILLIS / LSP_WINDOW_SIZE)
 //
 // Failure rules (as bitcoin/miner.py): an empty range (Lower > Upper) is answered with
-// (2^64-1, 2^64-1), the identity of the server's (hash, nonce) merge; GPUHASH_EINVAL /
-// GPUHASH_ETOOLONG are deterministic, so the job is logged and skipped; any other engine
-// error, or a result whose hash the host re-computation disagrees with, ends the miner
-// so the server requeues its job.  stdout is never written (the graders read it).
+// (2^64-1, 2^64-1), the identity of the server's (hash, nonce) merge; every engine error
+// -- GPUHASH_EINVAL / GPUHASH_ETOOLONG as much as a device error -- and a result whose
+// hash the host re-computation disagrees with ends the miner, so every Request gets
+// exactly one Result or a lost connection, which the server requeues (an argument error
+// fails each miner the same way until the server's requeue cap disconnects the client).
+// stdout is never written (the graders read it).
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
@@ -104,10 +106,9 @@ int main(int argc, char** argv) {
             uint64_t h = 0, n = 0;
             rc = gpuhash_min(ctx, reinterpret_cast<const uint8_t*>(m.data.data()), m.data.size(), m.lower,
                              m.upper, &h, &n);
-            if (rc == GPUHASH_EINVAL || rc == GPUHASH_ETOOLONG) {
-                logf("job %s skipped: %s", lspn::btc_describe(m).c_str(), gpuhash_strerror(rc));
-                continue;  // deterministic: every miner would fail it the same way
-            }
+            // No Result can be sent for a failed job, and skipping it would leave it in
+            // flight forever (the server pairs each Result with the miner's OLDEST job),
+            // so every error ends the miner and the server requeues the job.
             if (rc != GPUHASH_OK) {
                 logf("job %s: %s; exiting so the server requeues it", lspn::btc_describe(m).c_str(),
                      gpuhash_strerror(rc));

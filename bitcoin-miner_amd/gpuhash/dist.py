@@ -6,7 +6,9 @@ search contiguous shards with NO data-path collective; the only communication is
 final 16-byte result per rank, gathered once (the host-argmin step of the north_star,
 done across processes instead of across threads).
 
-  split_range   strong scaling: [lower, upper] cut into `world` contiguous shards
+  split_range   strong scaling: [lower, upper] cut into `world` contiguous shards; given
+                the message length, by the ENGINE's cost model (gpuhash_shard_range, the
+                same cut points gpuhash_min uses over devices), else by count
   weak_range    weak scaling: rank r searches [base + r*per_rank, base + (r+1)*per_rank)
   merge_min     lexicographic (hash, nonce) argmin -- lowest nonce on equal hashes
   distributed_min   shard -> local search -> all_gather(16 B) -> merge
@@ -18,10 +20,20 @@ from typing import Callable, Iterable
 U64_MAX = (1 << 64) - 1
 
 
-def split_range(lower: int, upper: int, world: int) -> list[tuple[int, int] | None]:
-    """Contiguous, equal-count shards of the inclusive range; None for an empty shard."""
+def split_range(lower: int, upper: int, world: int,
+                msg_len: int | None = None) -> list[tuple[int, int] | None]:
+    """Contiguous shards of the inclusive range, in rank order; None for an empty shard.
+
+    With msg_len, the shards are of equal estimated COST (for message
+    lengths 45-54 the digit groups differ in SHA blocks per nonce, so equal counts would
+    leave the 2-block ranks last): the cut points come from the C ABI,
+    gpuhash_shard_range, so in-process devices and processes shard identically.  Without
+    it, equal counts (a search function that is not the engine, e.g. the oracle)."""
     if lower > upper:
         raise ValueError("lower > upper")
+    if msg_len is not None:
+        from gpuhash import shard_range
+        return shard_range(msg_len, lower, upper, world)
     count = upper - lower + 1
     out: list[tuple[int, int] | None] = []
     start = lower
@@ -79,10 +91,10 @@ def gather_results(res: tuple[int, int] | None, device=None) -> list[tuple[int, 
 
 
 def distributed_min(search: Callable[[int, int], tuple[int, int]], lower: int, upper: int,
-                    device=None) -> tuple[int, int]:
+                    device=None, msg_len: int | None = None) -> tuple[int, int]:
     """Every rank searches its shard of [lower, upper] with `search(lo, hi)`; returns the
-    global argmin on every rank."""
+    global argmin on every rank.  msg_len selects the engine's cost-balanced split."""
     import torch.distributed as dist
-    shard = split_range(lower, upper, dist.get_world_size())[dist.get_rank()]
+    shard = split_range(lower, upper, dist.get_world_size(), msg_len)[dist.get_rank()]
     local = search(*shard) if shard is not None else None
     return merge_min(gather_results(local, device))

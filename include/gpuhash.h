@@ -94,6 +94,23 @@ int gpuhash_open(const int *devices, int ndevices, gpuhash_ctx **out);
 /* Number of devices a context drives. */
 int gpuhash_ndevices(const gpuhash_ctx *ctx);
 
+/* Number of visible HIP devices (0 if none).  Lets a host check a device list before
+ * gpuhash_open (bench.py --gpus N refuses N above it).  Replaces nothing in the reference. */
+int gpuhash_device_count(void);
+
+/* The static partition gpuhash_min applies over n devices, for hosts that shard one
+ * search over PROCESSES instead (gpuhash.dist: one process per GPU):
+ * nshards contiguous shards of the inclusive [lower, upper], in order, of equal estimated
+ * cost -- nonces x the layout's relative cost per digit group, so a range whose digit
+ * groups differ in SHA blocks (message lengths 45-54, 1 -> 2 blocks at some digit count)
+ * is balanced by work, not by count.  Shard k is [out_lower[k], out_upper[k]];
+ * out_lower[k] > out_upper[k] (1 > 0) marks an empty shard.  Returns the number of
+ * non-empty shards, or GPUHASH_EINVAL (nshards < 1, null outputs, lower > upper) /
+ * GPUHASH_ETOOLONG.  Host-only: needs no device.  Replaces the server's job split of
+ * p1.pdf p.14 within one node; the merge is the same (hash, nonce) argmin. */
+int gpuhash_shard_range(size_t msg_len, uint64_t lower, uint64_t upper, int nshards,
+                        uint64_t *out_lower, uint64_t *out_upper);
+
 /* Layout choice for nonces whose digits straddle two SHA blocks with 5-8 digits in the
  * last one: AUTO (default) takes the uniform-schedule layout when the
  * search fills its lane rows, UNIFORM always takes it, CLASSIC never.  Results are

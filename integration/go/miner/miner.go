@@ -62,15 +62,14 @@ func main() {
 		// was: for n := req.Lower; n <= req.Upper; n++ { h := bitcoin.Hash(req.Data, n) ... }
 		hash, nonce, err := eng.Min(req.Data, req.Lower, req.Upper)
 		if err != nil {
+			// Argument errors (ge.IsArgument) as much as device errors: no Result can be
+			// sent, and skipping the job would leave it in flight forever (the server
+			// pairs each Result with the miner's oldest job).  Exiting drops the
+			// connection, the server requeues the job (p1.pdf p.15), and its requeue cap
+			// disconnects the client if every miner fails it the same way.
 			var ge *gpuhash.Error
-			if errors.As(err, &ge) && ge.IsArgument() {
-				// deterministic: every miner would fail this job the same way, so skip it
-				// (logged to stderr; stdout is graded) instead of exiting, which would make
-				// the server requeue it to the next miner
-				log.Printf("miner: job %v skipped: %v", req, err)
-				continue
-			}
-			return // device error: exit, the server requeues the job (p1.pdf p.15)
+			log.Printf("miner: job %v failed (argument error: %v): %v; exiting", req, errors.As(err, &ge) && ge.IsArgument(), err)
+			return
 		}
 		// optional self-check against the unmodified reference hash
 		if bitcoin.Hash(req.Data, nonce) != hash {

@@ -8,8 +8,9 @@
  * GPU.  The product miner (bitcoin-miner_amd/lib/gpuhash_miner) links the real
  * libgpuhash.so; nothing under bitcoin-miner_amd/ builds or loads this file.
  *
- * Test hook: a message equal to "__gpuhash_test_ehip__" makes gpuhash_min return
- * GPUHASH_EHIP (a device error), so the miner's exit-and-requeue path can be driven.
+ * Test hooks: a message equal to "__gpuhash_test_ehip__" makes gpuhash_min return
+ * GPUHASH_EHIP (a device error), "__gpuhash_test_einval__" GPUHASH_EINVAL (an argument
+ * error), so the miner's exit-and-requeue paths can be driven over LSP.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -33,10 +34,11 @@ int gpuhash_open(const int *devices, int ndevices, gpuhash_ctx **out) {
 
 int gpuhash_min(gpuhash_ctx *ctx, const uint8_t *msg, size_t msg_len, uint64_t lower, uint64_t upper,
                 uint64_t *out_hash, uint64_t *out_nonce) {
-    static const char ehip[] = "__gpuhash_test_ehip__";
+    static const char ehip[] = "__gpuhash_test_ehip__", einval[] = "__gpuhash_test_einval__";
     if (!ctx || !out_hash || !out_nonce || (msg_len && !msg) || lower > upper) return GPUHASH_EINVAL;
     if (msg_len > GPUHASH_MAX_MSG) return GPUHASH_ETOOLONG;
     if (msg_len == sizeof ehip - 1 && memcmp(msg, ehip, msg_len) == 0) return GPUHASH_EHIP;
+    if (msg_len == sizeof einval - 1 && memcmp(msg, einval, msg_len) == 0) return GPUHASH_EINVAL;
     return oracle_min(msg, msg_len, lower, upper, out_hash, out_nonce) ? GPUHASH_EINVAL : GPUHASH_OK;
 }
 

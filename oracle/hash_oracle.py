@@ -13,6 +13,8 @@ Two independent CPU restatements live in oracle/:
     ascending scan of the inclusive [Lower, Upper], strict '<' (lowest nonce wins ties).
   * hash_oracle.c: a from-FIPS-180-4 C restatement of the same, fast enough for the
     2^32-nonce golden and for the CPU baseline.  `load_c_oracle()` builds/loads it.
+  * golden_scan.c: a third restatement on the x86 SHA extensions and AVX-512, only to
+    compute the goldens of searches of 2^36-2^40 nonces (`GoldenScan`).
 
 Both are pinned to the handout's known-answer values (p1.pdf p.12), see
 tests/test_oracle.py.
@@ -61,6 +63,7 @@ def build_c_oracle(force: bool = False) -> str:
         os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
         subprocess.check_call(["gcc", "-O2", "-fPIC", "-shared", "-pthread", "-o", LIB_PATH, src])
     build_cpu_baseline(force)
+    build_golden_scan(force)
     return LIB_PATH
 
 
@@ -147,6 +150,48 @@ class COracle:
         out = np.empty(count, dtype=np.uint64)
         self.lib.oracle_hash_range(msg, len(msg), lower, count, out.ctypes.data)
         return out
+
+
+GOLDEN_PATH = os.path.join(HERE, "build", "libgoldenscan.so")
+
+
+def build_golden_scan(force: bool = False) -> str:
+    """oracle/golden_scan.c: the SHA-NI / AVX-512 scanner for the large fixtures."""
+    src = os.path.join(HERE, "golden_scan.c")
+    if force or not os.path.exists(GOLDEN_PATH) or os.path.getmtime(GOLDEN_PATH) < os.path.getmtime(src):
+        os.makedirs(os.path.dirname(GOLDEN_PATH), exist_ok=True)
+        subprocess.check_call(["gcc", "-O3", "-msha", "-msse4.1", "-fPIC", "-shared", "-pthread",
+                               "-o", GOLDEN_PATH, src])
+    return GOLDEN_PATH
+
+
+class GoldenScan:
+    """ctypes view of oracle/build/libgoldenscan.so (large goldens only)."""
+
+    def __init__(self):
+        self.lib = ctypes.CDLL(build_golden_scan())
+        u64, sz, p = ctypes.c_uint64, ctypes.c_size_t, ctypes.c_char_p
+        self.lib.golden_available.restype = ctypes.c_int
+        self.lib.golden_hash.restype = u64
+        self.lib.golden_hash.argtypes = [p, sz, u64]
+        self.lib.golden_min.restype = ctypes.c_int
+        self.lib.golden_min.argtypes = [p, sz, u64, u64, ctypes.c_int, ctypes.c_int,
+                                        ctypes.POINTER(u64), ctypes.POINTER(u64)]
+
+    def available(self) -> bool:
+        return bool(self.lib.golden_available())
+
+    def hash(self, msg: bytes, nonce: int) -> int:
+        return int(self.lib.golden_hash(msg, len(msg), nonce))
+
+    def min(self, msg: bytes, lower: int, upper: int, threads: int = 1,
+            progress: bool = False) -> tuple[int, int]:
+        h, n = ctypes.c_uint64(), ctypes.c_uint64()
+        rc = self.lib.golden_min(msg, len(msg), lower, upper, threads, int(progress),
+                                 ctypes.byref(h), ctypes.byref(n))
+        if rc != 0:
+            raise ValueError(f"golden_min rc={rc}")
+        return int(h.value), int(n.value)
 
 
 def load_c_oracle() -> COracle:

@@ -1,0 +1,123 @@
+"""GPU: the N>1 paths with the HIP engine as the per-rank search.
+
+* gpuhash.dist.distributed_min over 2 gloo ranks that share the one GPU, each rank
+  searching its shard with its own gpuhash context, the shards cut by the engine's cost
+  model (gpuhash_shard_range), on ranges that cross 1 -> 2 SHA blocks -- against the oracle.
+* bench.py's two N-GPU modes, rehearsed on the one GPU: `--inproc 0,0` (one process, two
+  shards, one stream each) and torch.distributed.run with 2 ranks (GPUHASH_SHARE_GPU=1);
+  their merged result must equal one call over the same range.  And `--gpus N` with N
+  above the visible devices must fail loudly instead of measuring one GPU.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+M120 = (b"The quick brown fox jumps over the lazy dog. " * 3)[:120]
+# m = 45: 9-digit nonces hash 1 block, 10-digit ones 2 (an extra padding block);
+# m = 50: the same change at 4 -> 5 digits
+CASES = [(M120[:45], 10**9 - (1 << 22), 10**9 + (1 << 22)),
+         (M120[:50], 0, 3_000_000),
+         (M120, 9_999_000_000, 10_004_000_000),
+         (b"bradfitz", 0, 9999)]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    import gpuhash
+    import gpuhash.dist as gd
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = []
+    with gpuhash.Engine([0]) as eng:
+        for msg, lo, hi in CASES:
+            shard = gd.split_range(lo, hi, world, msg_len=len(msg))[rank]
+            res = gd.distributed_min(lambda a, b: eng.min(msg, a, b), lo, hi, msg_len=len(msg))
+            out.append((shard, res))
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_distributed_min_with_the_hip_engine(oracle):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for i, (msg, lo, hi) in enumerate(CASES):
+        want = oracle.min(msg, lo, hi, threads=8)
+        (s0, r0), (s1, r1) = res[0][i], res[1][i]
+        assert r0 == r1 == want, (msg, lo, hi)
+        assert s0[0] == lo and s1[1] == hi and s1[0] == s0[1] + 1  # contiguous cost-balanced shards
+    # the cost model moves the m = 45 cut past 10^9: the 2-block shard holds fewer nonces
+    (a0, b0), (a1, b1) = res[0][0][0], res[1][0][0]
+    assert b0 > 10**9 and (b0 - a0) > 1.2 * (b1 - a1)
+
+
+def _bench(args, env_extra=None, launcher=None, timeout=100):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.update(env_extra or {})
+    cmd = (launcher or [sys.executable]) + [os.path.join(ROOT, "bench.py"), *args]
+    return subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=timeout, cwd=ROOT)
+
+
+def test_bench_inproc_two_shards_on_one_gpu(engine):
+    r = _bench(["--inproc", "0,0", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "inproc2"
+    assert line["config"]["ranges"] == [[0, (2 << 32) - 1]]
+    assert tuple(line["result"]) == engine.min(b"bradfitz", 0, (2 << 32) - 1)
+    assert line["roofline"]["kernel"] == "k_scan<J=4,C2=0,EX=0,MODE=0>"
+    assert len(line["per_device"]) == 1  # both shards report device ordinal 0
+
+
+def test_bench_gpus_above_visible_fails_loudly():
+    import gpuhash
+    n = gpuhash.device_count() + 1
+    r = _bench(["--gpus", str(n), "--steps", "1", "--warmup", "0", "--no-cpu-baseline"])
+    assert r.returncode == 2 and "HIP device(s) are visible" in r.stderr
+    assert r.stdout.strip() == ""
+
+
+def test_bench_torchrun_two_ranks_on_one_gpu(engine):
+    port = _free_port()
+    launcher = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(port)]
+    r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"],
+               {"GPUHASH_SHARE_GPU": "1"}, launcher=launcher)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "dp2"
+    assert line["config"]["backend"] == "gloo"
+    # rank r searched [r*2^32, (r+1)*2^32): the merged result is the whole range's argmin
+    assert tuple(line["result"]) == engine.min(b"bradfitz", 0, (2 << 32) - 1)
+    # without GPUHASH_SHARE_GPU, a second rank on a 1-GPU box is refused
+    import gpuhash
+    if gpuhash.device_count() == 1:
+        r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"],
+                   launcher=launcher[:-1] + [str(_free_port())])
+        assert r.returncode != 0 and "LOCAL_RANK 1" in r.stderr

@@ -3,6 +3,9 @@ LSP/UDP on localhost (BASELINE configs 1 and 5, reduced in size for a 1-GPU box)
 
 Config 1: `server` + one miner + `client host:port bradfitz 9999` must print exactly
 "Result 1419516646206828 9898" (p1.pdf p.15 output format).
+Config 5 at full size (test_config5_full_size): 16 clients x [0, 2^36], 8 miners sharing
+the GPU, 10% drops on every role, a SIGKILLed miner; four clients checked against CPU
+goldens (oracle/golden_scan.c), the rest against a direct search + oracle re-hash.
 Config 5 (scaled): 8 clients, 4 miners sharing the GPU, lspnet read and write drops of
 10% on every role, and one miner SIGKILLed mid-job.  Every client's printed result must
 equal a direct search of its whole range, and the winner must re-hash (oracle) to the
@@ -198,3 +201,52 @@ def test_config5_scaled_drops_and_killed_miner(procs, engine, oracle):
     server.send_signal(signal.SIGTERM)
     log = server.communicate(timeout=30)[1]
     assert "lost; job [" in log and "requeued" in log, log[-2000:]  # the killed miner's job was re-run
+
+
+@pytest.mark.timeout(600)
+def test_config5_full_size(procs, engine, oracle, golden):
+    """BASELINE configs[4] at full size on the one GPU (p1.pdf pp.14-15): 16 concurrent
+    clients "client-00".."client-15", each Request(msg, 0, 2^36); 8 GPU-backed miners (4
+    Python, 4 compiled) sharing the GPU; lspnet read and write drops of 10% on every role;
+    one miner SIGKILLed mid-job, whose job must be re-run.  Clients 00/05/10/15 are
+    checked against the CPU goldens of tests/golden/make_golden.py --huge (SHA-NI /
+    AVX-512 restatement over the whole [0, 2^36]); the others against one direct engine
+    search of the same range, plus an oracle re-hash of every printed winner."""
+    import time as _t
+    gold = {r["name"]: r for r in golden["ranges"]}
+    port = free_port()
+    drops = dict(LSPNET_CLIENT_READ_DROP=10, LSPNET_CLIENT_WRITE_DROP=10,
+                 LSPNET_SERVER_READ_DROP=10, LSPNET_SERVER_WRITE_DROP=10)
+    server = procs.start([os.path.join(BIN, "server"), str(port)], env=env(GPUHASH_SERVER_LOG=1, **drops))
+    time.sleep(0.5)
+    miners = [procs.start([os.path.join(BIN, "miner"), f"127.0.0.1:{port}"], env=env(**drops))
+              for _ in range(4)]
+    miners += [start_native(procs, port, **drops) for _ in range(4)]
+    time.sleep(4.0)  # let the miners open the GPU and join
+    max_nonce = 1 << 36
+    t0 = _t.time()
+    clients = [procs.start([os.path.join(BIN, "client"), f"127.0.0.1:{port}", f"client-{i:02d}",
+                            str(max_nonce)], env=env(**drops)) for i in range(16)]
+    time.sleep(3.0)
+    miners[1].send_signal(signal.SIGKILL)  # mid-job (2^34-nonce jobs take ~4 s per miner here)
+    outs = [c.communicate(timeout=400)[0].strip() for c in clients]
+    wall = _t.time() - t0
+    checked_golden = 0
+    for i, out in enumerate(outs):
+        parts = out.split()
+        assert parts[0] == "Result", (i, out)
+        h, n = int(parts[1]), int(parts[2])
+        msg = f"client-{i:02d}".encode()
+        g = gold.get(f"cfg5_client-{i:02d}_2p36")
+        if g is not None:
+            assert (g["lower"], g["upper"]) == (0, max_nonce)
+            assert (h, n) == (g["hash"], g["nonce"]), i
+            checked_golden += 1
+        else:
+            assert (h, n) == engine.min(msg, 0, max_nonce), i
+        assert oracle.hash(msg, n) == h
+    assert checked_golden == 4
+    server.send_signal(signal.SIGTERM)
+    log = server.communicate(timeout=30)[1]
+    assert "lost; job [" in log and "requeued" in log, log[-2000:]
+    print(f"config 5 full size: 16 x 2^36 nonces in {wall:.1f} s = {16 * (max_nonce + 1) / wall / 1e9:.1f} GH/s")

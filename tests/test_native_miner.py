@@ -198,6 +198,24 @@ def test_device_error_exits_and_the_requeue_cap_disconnects_the_client(miners, o
     close_quietly(srv)
 
 
+def test_argument_error_exits_and_the_requeue_cap_disconnects_the_client(miners, oracle):
+    """an argument error (here the shim's EINVAL hook, which the
+    server's validation cannot see) must not leave the job in flight: each miner exits,
+    the job is requeued until the cap, and the client prints Disconnected."""
+    lines = []
+    srv = start_server(job_size=1000, log=lines.append)
+    doomed = [miners.start(srv.port) for _ in range(4)]
+    time.sleep(0.5)
+    assert bclient.request(f"127.0.0.1:{srv.port}", "__gpuhash_test_einval__", 999, P) is None
+    for p in doomed:
+        assert p.wait(30) == 1
+        assert "exiting so the server requeues it" in p.stderr.read()
+    assert any("abandoned" in ln for ln in lines), lines
+    miners.start(srv.port)
+    assert bclient.request(f"127.0.0.1:{srv.port}", "bradfitz", 9999, P) == (1419516646206828, 9898)
+    close_quietly(srv)
+
+
 class BareServer:
     """A bare LSP server standing in for the bitcoin server: hands out raw payloads."""
 

@@ -131,3 +131,46 @@ def test_cpu_baseline_matches_the_oracle(oracle):
     assert b.min(b"bradfitz", 0, 200_000, threads=7) == oracle.min(b"bradfitz", 0, 200_000)
     with pytest.raises(ValueError):
         b.min(b"x", 5, 4)
+
+
+@pytest.fixture(scope="module")
+def golden_scan():
+    gs = ho.GoldenScan()
+    if not gs.available():
+        pytest.skip("no x86 SHA extensions on this host")
+    return gs
+
+
+def test_golden_scan_matches_the_oracle(golden_scan, oracle):
+    """oracle/golden_scan.c (SHA-NI midstates + AVX-512 or SHA-NI scan), which computes
+    the HUGE fixtures, against the plain-C oracle: KATs, random single hashes, and range
+    argmins over every digit count, block straddles, 1..3 threads (chunks of 2^22 never
+    split these, so the segment loop, the lane padding and the digit carries are what is
+    checked) and one range of several chunks."""
+    for msg, n, h in ho.SPEC_KATS:
+        assert golden_scan.hash(msg, n) == h
+    rng = random.Random(11)
+    for _ in range(1500):
+        m = bytes(rng.randrange(256) for _ in range(rng.randrange(0, 200)))
+        n = rng.choice([rng.randrange(1 << 64), rng.randrange(10 ** rng.randrange(1, 20))])
+        assert golden_scan.hash(m, n) == oracle.hash(m, n), (m, n)
+    for _ in range(150):
+        m = bytes(rng.randrange(32, 127) for _ in range(rng.randrange(0, 140)))
+        lo = rng.randrange(10 ** rng.randrange(1, 20))
+        hi = min(lo + rng.randrange(0, 3000), (1 << 64) - 1)
+        assert golden_scan.min(m, lo, hi, threads=rng.randrange(1, 4)) == oracle.min(m, lo, hi), (m, lo, hi)
+    assert golden_scan.min(b"bradfitz", 0, 9999) == (1419516646206828, 9898)
+    assert golden_scan.min(b"msg", (1 << 64) - 70, (1 << 64) - 1) == oracle.min(b"msg", (1 << 64) - 70, (1 << 64) - 1)
+    lo, hi = 10**9 - 5_000_000, 10**9 + 5_000_000  # 3 chunks, 9 -> 10 digits
+    assert golden_scan.min(b"client-03", lo, hi, threads=4) == oracle.min(b"client-03", lo, hi, threads=8)
+
+
+def test_huge_goldens_rehash(golden, oracle):
+    """Every HUGE fixture's winner re-hashes to its hash under the two other
+    restatements (the full ranges are the GPU tests' job)."""
+    huge = [r for r in golden["ranges"] if "computed_by" in r]
+    assert len(huge) >= 3
+    for r in huge:
+        m = bytes.fromhex(r["msg_hex"])
+        assert r["lower"] <= r["nonce"] <= r["upper"]
+        assert oracle.hash(m, r["nonce"]) == r["hash"] == ho.hash_py(m, r["nonce"]), r["name"]

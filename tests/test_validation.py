@@ -193,7 +193,11 @@ def _device_error():
     return e
 
 
-def test_miner_answers_empty_range_and_skips_argument_errors(oracle):
+def test_miner_answers_empty_range_and_exits_on_argument_errors(oracle):
+    """every Request gets exactly one Result or a lost connection.
+    The stub server here does NOT validate, so the argument error reaches the engine; the
+    miner must not skip the job (it would stay in flight, and with two jobs per miner the
+    next Result would answer the wrong request) but exit, so the job is requeued."""
     s = _Server()
 
     class Eng:
@@ -210,14 +214,67 @@ def test_miner_answers_empty_range_and_skips_argument_errors(oracle):
     s.srv.Write(conn, bitcoin.marshal(bitcoin.NewRequest("msg", 5, 4)))
     r = s.result()
     assert (r.Type, r.Hash, r.Nonce) == (bitcoin.MsgType.Result, U64, U64)
-    s.srv.Write(conn, bitcoin.marshal(bitcoin.NewRequest("bad", 0, 9)))  # skipped, miner lives
     s.srv.Write(conn, bitcoin.marshal(bitcoin.NewRequest("msg", 0, 2)))
     r = s.result()
     assert (r.Hash, r.Nonce) == (4754799531757243342, 1)  # p1.pdf p.12
-    assert th.is_alive()
-    s.srv.Close()
+    s.srv.Write(conn, bitcoin.marshal(bitcoin.NewRequest("bad", 0, 9)))  # -> exit, no Result
+    s.srv.Write(conn, bitcoin.marshal(bitcoin.NewRequest("msg", 0, 2)))  # queued, never served
     th.join(10)
-    assert rc.get("rc") == 0
+    assert not th.is_alive() and rc.get("rc") == 1
+    # the server side sees the connection lost, never a Result for the failed job
+    with pytest.raises(lsp.LSPError):
+        s.result()
+    try:
+        s.srv.Close()
+    except lsp.LSPError:
+        pass
+
+
+def test_argument_error_on_every_miner_hits_the_requeue_cap(oracle):
+    """The real server with its request validation bypassed (so a job the engine refuses
+    reaches the miners): each miner exits on it, the job is requeued, and after
+    MAX_REQUEUES the client sees Disconnected instead of hanging; the server goes on."""
+    from bitcoin import client as bclient
+    from bitcoin import server as bserver
+    box, ready, lines = {}, threading.Event(), []
+    orig = bserver.request_error
+    bserver.request_error = lambda *a, **k: None  # a server that does not validate
+    try:
+        def on_ready(srv):
+            box["srv"] = srv
+            ready.set()
+        threading.Thread(target=bserver.serve, args=(0,),
+                         kwargs=dict(params=P, job_size=1000, ready=on_ready, log=lines.append),
+                         daemon=True).start()
+        ready.wait(5)
+        port = box["srv"].port
+
+        class Eng:
+            def min(self, msg, lo, hi):
+                if msg == "bad":
+                    raise _argument_error()
+                return oracle.min(msg.encode(), lo, hi)
+
+        rcs = []
+        ths = [threading.Thread(target=lambda: rcs.append(bminer.run(f"127.0.0.1:{port}", Eng(), P)), daemon=True)
+               for _ in range(bserver.MAX_REQUEUES + 1)]
+        for t in ths:
+            t.start()
+        time.sleep(0.3)
+        assert bclient.request(f"127.0.0.1:{port}", "bad", 99, P) is None  # Disconnected
+        for t in ths:
+            t.join(30)
+        assert rcs == [1] * (bserver.MAX_REQUEUES + 1)
+        assert any("abandoned" in ln for ln in lines), lines
+        # the server still serves a good request with a healthy miner
+        threading.Thread(target=lambda: bminer.run(f"127.0.0.1:{port}", Eng(), P), daemon=True).start()
+        assert bclient.request(f"127.0.0.1:{port}", "bradfitz", 9999, P) == (1419516646206828, 9898)
+    finally:
+        bserver.request_error = orig
+        try:
+            box["srv"].Close()
+        except (lsp.LSPError, KeyError):
+            pass
 
 
 def test_miner_exits_on_device_error():
