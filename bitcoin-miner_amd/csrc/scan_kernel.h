@@ -355,8 +355,17 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
                 x.h = x.g; x.g = x.f; x.f = x.e; x.e = (x.d + inv) + WJ;
                 x.d = x.c; x.c = x.b; x.b = x.a; x.a = (inv + t2) + WJ;
             }
+#ifdef GPUHASH_EXTRA_SALU
+            // tuning probe (tools/build_salu_variants.sh, never in the product build): one
+            // extra scalar instruction per round from round 20 on -- as many as the K
+            // constants the loop re-materialises with s_mov_b32 -- to price those s_movs
+            uint32_t salu_dummy = __builtin_amdgcn_readfirstlane(r);
+#endif
             sfor<J + 1, 63>([&](auto tc) {
                 constexpr int t = decltype(tc)::value;
+#ifdef GPUHASH_EXTRA_SALU
+                if constexpr (t >= 20) asm volatile("s_xor_b32 %0, %0, %1" : "+s"(salu_dummy) : "i"(K[t]));
+#endif
                 if constexpr (t < 16) {
                     round_kw(x, K[t] + w[t]);   // uniform word: K+W folds
                 } else {
