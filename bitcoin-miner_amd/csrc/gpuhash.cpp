@@ -211,15 +211,18 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
     }
 
     // meta layout: [per group: work counter + 4 clock words, 40 B][per group: offs
-    // (n+1) x 8 B, descs]
+    // (n+1) x 8 B, descs, and for C2 = 3 the launches' p-tables]
     size_t bytes = kCounterBytes * groups.size();
-    std::vector<size_t> offs_at(groups.size()), desc_at(groups.size());
+    std::vector<size_t> offs_at(groups.size()), desc_at(groups.size()), ptab_at(groups.size());
     for (size_t g = 0; g < groups.size(); g++) {
         offs_at[g] = bytes;
         bytes += 8 * (groups[g].idx.size() + 1);
         bytes = (bytes + 15) & ~(size_t)15;
         desc_at[g] = bytes;
         bytes += sizeof(LaunchDesc) * groups[g].idx.size();
+        bytes = (bytes + 15) & ~(size_t)15;
+        ptab_at[g] = bytes;
+        for (size_t k : groups[g].idx) bytes += sizeof(uint32_t) * plan[k].ptab.size();
         bytes = (bytes + 15) & ~(size_t)15;
     }
     int rc = dev_reserve_meta(d, bytes);
@@ -235,6 +238,8 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
     for (size_t g = 0; g < groups.size(); g++) {
         auto* offs = reinterpret_cast<unsigned long long*>(d.h_meta + offs_at[g]);
         auto* descs = reinterpret_cast<LaunchDesc*>(d.h_meta + desc_at[g]);
+        auto* ptabs = reinterpret_cast<uint32_t*>(d.h_meta + ptab_at[g]);
+        uint32_t ptab_words = 0;
         unsigned long long acc = 0;
         for (size_t k = 0; k < groups[g].idx.size(); k++) {
             const Launch& l = plan[groups[g].idx[k]];
@@ -242,6 +247,11 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
             offs[k] = acc;
             acc += (unsigned long long)((D.p_last - D.p_first) / (uint32_t)kBlock + 1u) * D.R;
             descs[k] = D;
+            if (l.C2 == 3) {  // lane table: this launch's p-table, after the group's descs
+                std::memcpy(ptabs + ptab_words, l.ptab.data(), sizeof(uint32_t) * l.ptab.size());
+                descs[k].tab_off = ptab_words;
+                ptab_words += (uint32_t)l.ptab.size();
+            }
             if (l.C2 == 1 && l.J == 0) {
                 auto it = std::find_if(tabs.begin(), tabs.end(), [&](const Tab& t) { return t.d == l.d; });
                 if (it == tabs.end()) {
@@ -295,7 +305,7 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
         a.ncand = d.d_ncand;
         a.dump = d_dump;
         a.dump_lo = lo;
-        a.ktab = d.d_ktab;
+        a.ktab = groups[g].C2 == 3 ? reinterpret_cast<const uint32_t*>(d.d_meta + ptab_at[g]) : d.d_ktab;
         a.grid = grids[g];
         HIPCHK(hipEventRecord(d.ev[2 * g], a.stream));
         HIPCHK(launch_scan(groups[g].J, groups[g].C2, groups[g].EX, mode, a));
@@ -411,7 +421,7 @@ int gpuhash_shard_range(size_t msg_len, uint64_t lower, uint64_t upper, int nsha
 }
 
 int gpuhash_set_layout_policy(gpuhash_ctx* ctx, int policy) {
-    if (!ctx || policy < GPUHASH_LAYOUT_AUTO || policy > GPUHASH_LAYOUT_CLASSIC) return GPUHASH_EINVAL;
+    if (!ctx || policy < GPUHASH_LAYOUT_AUTO || policy > GPUHASH_LAYOUT_LANETABLE) return GPUHASH_EINVAL;
     std::lock_guard<std::mutex> lock(ctx->mu);
     ctx->policy = policy;
     return GPUHASH_OK;

@@ -83,6 +83,25 @@ int hostcheck_desc_hash(const uint8_t* msg, uint64_t len, uint64_t lower, uint64
     const Launch& l = v[(size_t)idx];
     const LaunchDesc& D = l.desc;
     if (nonce < l.lo || nonce > l.hi) return -2;
+    if (l.C2 == 3) {
+        // lane table: x = lane value (W_0/W_1 digits), r = loop value (p-table entry)
+        const uint64_t off = nonce - D.base;
+        const uint32_t r = (uint32_t)(off / D.RQ), x = (uint32_t)(off % D.RQ);
+        if (x < D.p_first || x > D.p_last || r >= D.R) return -3;  // not a rectangle
+        const uint32_t* P = &l.ptab[16ull * r];
+        uint32_t W[64], st[8];
+        std::memcpy(W, D.U, 64);
+        W[0] |= ascii4(x / D.R1);
+        W[1] |= (ascii4(x % D.R1) & D.qmask) << D.loop_shift;
+        sha256_expand(W);
+        std::memcpy(st, P, 32);
+        // round 0 from the table's partial sums (as the kernel's ut_hash), then 1..63
+        const uint32_t kw0 = kK[0] + W[0];
+        uint32_t s1[8] = {P[8] + P[9] + kw0, st[0], st[1], st[2], st[3] + P[8] + kw0, st[4], st[5], st[6]};
+        sha256_rounds(s1, W, 1, 64);
+        *out = ((uint64_t)(P[0] + s1[0]) << 32) | (uint32_t)(P[1] + s1[1]);
+        return 0;
+    }
     const uint64_t off = nonce - D.base;
     const uint32_t p = (uint32_t)(off / D.R), r = (uint32_t)(off % D.R);
     const uint32_t alo = ascii4(p % 10000u), ahi = ascii4((p / 10000u) % 10000u);

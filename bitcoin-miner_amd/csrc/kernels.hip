@@ -76,6 +76,7 @@ static unsigned int occ(int device) {
 // Expands a runtime (J, C2, EX) into the matching template instance and applies F.
 template <int MODE, class F>
 static auto with_variant(int J, int C2, int EX, F&& f) {
+    if (C2 == 3) return f.template operator()<1, 3, false, MODE>();
     if (C2 == 2) return f.template operator()<1, 2, false, MODE>();
     if (C2) {
         switch (J) {
@@ -109,7 +110,7 @@ static auto with_variant(int J, int C2, int EX, F&& f) {
 }
 
 static bool valid_variant(int J, int C2, int EX) {
-    if (C2 == 2) return !EX && J == 1;
+    if (C2 == 2 || C2 == 3) return !EX && J == 1;
     if (C2) return C2 == 1 && !EX && (J == 0 || J == 1);
     if (EX) return J >= 13 && J <= 15;
     return J >= 0 && J <= 13;  // J = 14, 15 always need the extra block

@@ -1,5 +1,6 @@
 // kernels_ut.hip -- k_scan instances of the K+W-table uniform-schedule layout (C2 = 1,
-// J = 0: block B holds loop digits only) and the table builder k_ktab.
+// J = 0: block B holds loop digits only), the lane-table layout (C2 = 3,
+// J = 1) and the table builder k_ktab.
 // Built with -mllvm -amdgpu-sched-strategy=max-ilp (Makefile): +2.1% on config 3 over
 // the default options (profiles/r01_variants.jsonl).
 #include "scan_decl.h"
@@ -29,3 +30,6 @@ __global__ __launch_bounds__(256) void k_ktab(const LaunchDesc* __restrict__ des
 
 GPUHASH_INSTANTIATE_SCAN(0, 1, false, 0);
 GPUHASH_INSTANTIATE_SCAN(0, 1, false, 1);
+// C2 = 3: the lane-table straddle layout (scan_row_lt), uniform-table family too
+GPUHASH_INSTANTIATE_SCAN(1, 3, false, 0);
+GPUHASH_INSTANTIATE_SCAN(1, 3, false, 1);

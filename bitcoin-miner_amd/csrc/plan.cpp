@@ -158,11 +158,23 @@ GroupLayout layout_for(uint64_t m, int d, uint64_t span = 0, int policy = kLayou
             const double cost = (double)full + (full ? kLastRow[busy] : kOneRow[busy]);
             fill_ok = (double)lanes / (kBlock * cost) >= 0.70;
         }
+        if (policy == kLayoutLaneTable) fill_ok = false;
         if (nb1 >= 3 && fill_ok) {
             g.C2 = 2;
             g.q1 = g.q;
             g.q = 4 + g.q;
             g.s = std::min(std::min(kMaxLane, nb1), kMaxLaunchDigitsU2 - g.q);
+        } else if (policy != kLayoutClassic) {
+            // C2 = 3 (lane table): block B still carries loop-free digits only, but the
+            // LANES take its 4 + q1 digits (>= 10^5 values: rows always fill) and keep its
+            // schedule in registers, while the loop runs over the few block B-1 values
+            // the rows of C2 = 2 could not fill (1-2 digits, or a narrow search).  A nonce
+            // then costs block B's 64 rounds, as in C2 = 2, against a full per-nonce
+            // schedule in the classic layout.
+            g.C2 = 3;
+            g.q1 = g.q;
+            g.q = 4 + g.q;
+            g.s = std::min(kMaxLane, nb1);
         }
     }
     return g;
@@ -252,10 +264,52 @@ void build_launch(const uint8_t* msg, uint64_t m, const Prefix& pre, const Group
     }
     D.mask_lo = low_bytes_mask(std::min(s, 4));
     D.mask_hi = low_bytes_mask(s - 4);
-    D.qmask = low_bytes_mask(g.C2 == 2 ? g.q1 : q);
-    D.R1 = g.C2 == 2 ? (uint32_t)pow10u(g.q1) : 1u;
+    D.qmask = low_bytes_mask(g.C2 >= 2 ? g.q1 : q);
+    D.R1 = g.C2 >= 2 ? (uint32_t)pow10u(g.q1) : 1u;
     const int e = (int)((L - 1) % 64);
     D.loop_shift = (uint32_t)(3 - e % 4) * 8u;
+    if (g.C2 == 3) {
+        // lane table: lanes = the q digits of W_0/W_1 (x in [x_a, x_b]), loop = the s digits
+        // at the end of block B-1 (p in [p_a, p_b]); [lo, hi] is a rectangle (plan_range)
+        const uint64_t U = pow10u(s + q), RQ = pow10u(q);
+        const uint64_t off_lo = lo - H * U, off_hi = hi - H * U;
+        const uint64_t p_a = off_lo / RQ, p_b = off_hi / RQ;
+        const uint32_t NP = (uint32_t)(p_b - p_a + 1);
+        D.RQ = (uint32_t)RQ;
+        D.R = NP;
+        D.rchunk = NP;
+        D.nrchunks = 1;
+        D.p_first = (uint32_t)(off_lo % RQ);
+        D.p_last = (uint32_t)(off_hi % RQ);
+        D.r_first = 0;
+        D.r_last = NP - 1u;
+        D.base = H * U + p_a * RQ;
+        // p-table: block B-1 with the s loop digits of p (its last s bytes), compressed
+        // from CV1, then round 0 of block B up to its K+W term
+        out.ptab.assign(16ull * NP, 0u);
+        std::vector<uint8_t> blk(64);
+        std::memcpy(blk.data(), &buf[(g.B - 1 - p0) * 64], 64);
+        for (uint32_t k = 0; k < NP; k++) {
+            uint64_t v = p_a + k;
+            for (int i = s - 1; i >= 0; i--) { blk[64 - (size_t)s + (size_t)i] = (uint8_t)('0' + v % 10u); v /= 10u; }
+            uint32_t w[16], cv[8];
+            for (int i = 0; i < 16; i++) w[i] = be32(&blk[4 * (size_t)i]);
+            std::memcpy(cv, D.CV1, 32);
+            sha256_compress(cv, w);
+            uint32_t* e8 = &out.ptab[16ull * k];
+            std::memcpy(e8, cv, 32);
+            const uint32_t a = cv[0], b = cv[1], c = cv[2], ee = cv[4], f = cv[5], gg = cv[6], h = cv[7];
+            e8[8] = h + (ror(ee, 6) ^ ror(ee, 11) ^ ror(ee, 25)) + ((ee & f) ^ (~ee & gg));
+            e8[9] = (ror(a, 2) ^ ror(a, 13) ^ ror(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+        }
+        out.J = g.J; out.C2 = g.C2; out.EX = g.EX;
+        out.d = d; out.q = q; out.s = s;
+        out.c = 2;
+        out.lo = lo; out.hi = hi;
+        out.nblocks = (D.p_last - D.p_first) / (uint32_t)kBlock + 1u;
+        return;
+    }
+    out.ptab.clear();
     const uint64_t R = pow10u(q), P = pow10u(s);
     D.R = (uint32_t)R;
     // r values per work item: ~100 keeps every workgroup short (a few ms at full load)
@@ -296,9 +350,34 @@ void plan_range(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper
         for (uint64_t H = Hf;; H++) {
             uint64_t lo = std::max(a, H * U);
             uint64_t hi = (H == Hl) ? b : H * U + (U - 1);
-            Launch l;
-            build_launch(msg, len, pre, g, H, lo, hi, rchunk_max, l);
-            out.push_back(l);
+            if (g.C2 == 3) {
+                // lane table: each launch must be a rectangle (loop values p) x (lane
+                // values x) -- a partial first p, the full p's, a partial last p -- of at
+                // most kMaxLtLoop p values
+                const uint64_t RQ = pow10u(g.q), base = H * U;
+                uint64_t o = lo - base;
+                const uint64_t oe = hi - base;
+                while (o <= oe) {
+                    const uint64_t p = o / RQ, x = o % RQ;
+                    uint64_t end;  // last offset of this rectangle
+                    if (x != 0 || oe / RQ == p) {
+                        end = std::min(oe, p * RQ + RQ - 1);  // within one p
+                    } else {
+                        uint64_t pe = oe / RQ;  // full p's up to pe (pe's row may be partial)
+                        if (oe % RQ != RQ - 1) pe--;
+                        pe = std::min(pe, p + kMaxLtLoop - 1);
+                        end = pe * RQ + RQ - 1;
+                    }
+                    Launch l;
+                    build_launch(msg, len, pre, g, H, base + o, base + end, rchunk_max, l);
+                    out.push_back(std::move(l));
+                    o = end + 1;
+                }
+            } else {
+                Launch l;
+                build_launch(msg, len, pre, g, H, lo, hi, rchunk_max, l);
+                out.push_back(std::move(l));
+            }
             if (H == Hl) break;
         }
     }
@@ -312,7 +391,8 @@ double group_cost(uint64_t msg_len, int d) {
     // uniform-schedule C2 ~45, extra padding block ~20.5)
     double c = 1.0;
     if (g.EX) c += 0.7;
-    if (g.C2 == 2 || (g.C2 == 1 && g.J == 0)) c = 0.75;
+    if (g.C2 == 2 || g.C2 == 3 || (g.C2 == 1 && g.J == 0)) c = 0.75;
+    if (g.C2 == 3) return c + 0.6 / (double)pow10u(g.s);  // per-row schedule over the loop
     if (g.C2) c += 0.9 / (double)pow10u(g.q);
     else c += 0.2 / (double)std::min<uint64_t>(pow10u(g.q), 100);
     return c;

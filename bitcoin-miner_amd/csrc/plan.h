@@ -16,6 +16,12 @@
 //     (C2 = 2, J = 1: the loop takes the 4 digits of W_0 as well -- q = 4 + digits of
 //      W_1, up to 8 -- so block B holds loop digits only and its schedule is uniform;
 //      the lanes then take only digits of block B-1)
+//     (C2 = 3, J = 1, "lane table": the roles swap -- each LANE takes one value of the
+//      q = 4 + q1 digits of block B's W_0/W_1 and keeps that block's whole K+W schedule
+//      in registers, built once per row; the LOOP runs over the s digits at the end of
+//      block B-1, whose chaining values the host precomputes (16 words per value, the
+//      launch's "p-table").  For straddles whose block B-1 holds too few digits to fill
+//      C2 = 2's 256-lane rows, e.g. message lengths = 61, 62 mod 64 at 6-10 digits)
 //     uniform     : prefix bytes, H's digits, 0x80, zero pad, bit length -> host
 //                    precomputes the midstate, the uniform words and the rounds that
 //                    only read uniform words
@@ -60,9 +66,11 @@ struct LaunchDesc {
     // B-1), so its whole schedule K[t] + W_t(r) is a per-r table, built once per digit
     // group by k_ktab; the scan reads row r at ktab + tab_off + 64*r (scalar loads).
     uint32_t tab_off;
-    uint32_t R1;       // C2 = 2: 10^(digits of W_1); r = (W_0 digits) * R1 + (W_1 digits)
-    uint32_t pad_;
-    uint64_t base;     // nonce = base + p·R + r
+    // C2 = 3: tab_off = word offset of this launch's p-table (16 words per loop value:
+    // block B-1's chaining value, then round 0's per-row sums inv0 and t20 of block B)
+    uint32_t R1;       // C2 = 2, 3: 10^(digits of W_1); (W_0, W_1) digits = (x / R1, x % R1)
+    uint32_t RQ;       // C2 = 3: 10^q, lane values per loop value
+    uint64_t base;     // nonce = base + p·R + r  (C2 = 3: base + r·RQ + p, p = lane value)
 };
 
 struct Launch {
@@ -74,6 +82,7 @@ struct Launch {
     uint64_t lo, hi;      // inclusive nonce range covered
     uint32_t nblocks;     // grid size (workgroups of 256)
     LaunchDesc desc;
+    std::vector<uint32_t> ptab;  // C2 = 3: 16 words per loop value (LaunchDesc::tab_off)
 };
 
 // Largest number of lane digits; 10^kMaxLane lanes per launch.
@@ -83,12 +92,15 @@ static constexpr int kMaxLaunchDigits = 10;   // s + q <= 10  -> <= 10^10 nonces
 // C2 = 2 launches: s + q <= 12 still keeps rows * R = ceil(10^s / 256) * 10^q < 2^32
 static constexpr int kMaxLaunchDigitsU2 = 12;
 
-// Choice between the two J = 1 straddling layouts (plan.cpp layout_for):
-//   auto     C2 = 2 (uniform two-word loop) when its measured partial-row cost model
-//            predicts it beats the classic layout (plan.cpp)
-//   uniform  C2 = 2 whenever block B-1 holds >= 3 digits (tuning / parity tests)
-//   classic  never C2 = 2
-enum LayoutPolicy { kLayoutAuto = 0, kLayoutUniform = 1, kLayoutClassic = 2 };
+// Choice between the J = 1 straddling layouts (plan.cpp layout_for):
+//   auto       C2 = 2 (uniform two-word loop) when its measured partial-row cost model
+//              predicts full enough rows, else C2 = 3 (lane table)
+//   uniform    C2 = 2 whenever block B-1 holds >= 3 digits, else C2 = 3 (tuning / tests)
+//   classic    C2 = 1: lanes in W_0 and block B-1, per-nonce schedule (tuning / tests)
+//   lanetable  C2 = 3 always (tuning / tests)
+enum LayoutPolicy { kLayoutAuto = 0, kLayoutUniform = 1, kLayoutClassic = 2, kLayoutLaneTable = 3 };
+// C2 = 3: at most this many loop values (p-table entries) per launch
+static constexpr uint32_t kMaxLtLoop = 1024;
 
 // Plans [lower, upper] (inclusive, lower <= upper) of `msg`.  `rchunk_max` caps the r
 // values per work item (0 = default).  Appends to `out`.

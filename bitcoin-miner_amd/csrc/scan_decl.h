@@ -3,7 +3,8 @@
 // The k_scan instances are compiled in three TUs with the code-generation options each
 // layout family measured best with (tools/variant_bench.py):
 //   kernels_plain.hip  C2 = 0, no extra block: 8 waves/SIMD (63 VGPRs, no spills)
-//   kernels_ut.hip     C2 = 1, J = 0 (K+W table layouts) + k_ktab: max-ILP scheduling
+//   kernels_ut.hip     C2 = 1, J = 0 (K+W table layouts), C2 = 3 (lane table) + k_ktab:
+//                      max-ILP scheduling
 //   kernels_misc.hip   C2 = 1/J = 1, C2 = 2, extra-block layouts: max-ILP scheduling
 // kernels.hip launches them through these declarations only, so nothing is implicitly
 // instantiated there.

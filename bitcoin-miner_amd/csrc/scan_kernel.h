@@ -397,6 +397,73 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
     }
 }
 
+// C2 = 3 (lane table): one row = 256 consecutive values x of block B's W_0/W_1 digits,
+// one per lane, x loop values r = the block B-1 digits, p = p_a + r.  Per row each lane
+// builds block B's K+W schedule for its x ONCE (kept in registers: the rows of C2 = 2
+// could share one schedule across a wave only because its lanes varied block B-1); per
+// loop value the wave reads block B-1's chaining value and round 0's partial sums from
+// the host's p-table (scalar loads) and every lane runs block B's 64 rounds, as ut_hash.
+// nonce = D.base + r * D.RQ + x.
+template <int MODE>
+__device__ __forceinline__ void scan_row_lt(const LaunchDesc& D, uint32_t row, uint32_t r0, uint32_t r1,
+                                            WaveBest& wb, unsigned long long* __restrict__ dump,
+                                            unsigned long long dump_lo, const uint32_t* __restrict__ ptab) {
+    using namespace dev;
+    const uint32_t x = D.p_first + row * 256u + threadIdx.x;
+    const bool wave_idle =
+        __builtin_amdgcn_readfirstlane(D.p_first + row * 256u + (threadIdx.x & ~63u)) > D.p_last;
+    if (wave_idle) return;
+    const bool lane_ok = x <= D.p_last;
+    uint32_t kw[64];
+    {
+        const uint32_t hi4 = x / D.R1, lo = x - hi4 * D.R1;
+        uint32_t w[64];
+#pragma unroll
+        for (int i = 0; i < 16; i++) w[i] = D.U[i];
+        w[0] |= ascii4(hi4);
+        w[1] |= (ascii4(lo) & D.qmask) << D.loop_shift;
+        expand_full(w);
+#pragma unroll
+        for (int t = 0; t < 64; t++) kw[t] = K[t] + w[t];
+    }
+#pragma unroll 1
+    for (uint32_t r = r0; r < r1; r++) {
+        const uint32_t* __restrict__ P = ptab + D.tab_off + 16u * r;
+        uint32_t cv[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) cv[i] = P[i];
+        const State s{cv[0], cv[1], cv[2], cv[3], cv[4], cv[5], cv[6], cv[7]};
+        uint32_t H0, H1;
+        ut_hash(s, cv, P[8], P[9], [&](int t) { return kw[t]; }, H0, H1);
+#ifdef GPUHASH_TIE_TEST_BITS
+        H0 >>= (32 - GPUHASH_TIE_TEST_BITS);
+        H1 = 0;
+#endif
+        if constexpr (MODE == 1) {
+            if (lane_ok) dump[D.base + (unsigned long long)r * D.RQ + x - dump_lo] = ((unsigned long long)H0 << 32) | H1;
+        } else {
+            unsigned long long m = __builtin_amdgcn_ballot_w64(H0 <= wb.T);
+            if (m) {  // wave-uniform, rare once T has settled
+                m = __builtin_amdgcn_ballot_w64(H0 <= wb.T && lane_ok);
+                while (m) {
+                    const int l = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const uint32_t h0 = __builtin_amdgcn_readlane(H0, l);
+                    const uint32_t h1 = __builtin_amdgcn_readlane(H1, l);
+                    const uint32_t xl = __builtin_amdgcn_readlane(x, l);
+                    const unsigned long long hh = ((unsigned long long)h0 << 32) | h1;
+                    const unsigned long long nn = D.base + (unsigned long long)r * D.RQ + xl;
+                    if (hh < wb.h || (hh == wb.h && nn < wb.n)) {
+                        wb.h = hh;
+                        wb.n = nn;
+                        wb.T = h0 < wb.T ? h0 : wb.T;
+                    }
+                }
+            }
+        }
+    }
+}
+
 __device__ __forceinline__ unsigned long long uniform64(unsigned long long v) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
@@ -433,6 +500,7 @@ __global__ __launch_bounds__(256) GPUHASH_SCAN_ATTR void k_scan(const LaunchDesc
     static_assert(J >= 0 && J < 16, "loop word index");
     static_assert(!C2 || J <= 1, "C2 layouts have the loop word at J <= 1");
     static_assert(C2 != 2 || J == 1, "two-word uniform loop only with the loop word at J = 1");
+    static_assert(C2 != 3 || (J == 1 && !EX), "lane table only with the loop word at J = 1");
     static_assert(!EX || J >= 13, "extra padding block only when the last digit is at byte >= 55");
     __shared__ unsigned long long sh_grab[2];
     __shared__ unsigned long long sh_best[4][2];
@@ -477,7 +545,8 @@ __global__ __launch_bounds__(256) GPUHASH_SCAN_ATTR void k_scan(const LaunchDesc
             const uint32_t row = rel / D.R, r0 = rel - row * D.R;
             const unsigned long long left = end - x;
             const uint32_t r1 = (unsigned long long)(D.R - r0) < left ? D.R : r0 + (uint32_t)left;
-            scan_row<J, C2, EX, MODE>(D, row, r0, r1, wb, dump, dump_lo, ktab);
+            if constexpr (C2 == 3) scan_row_lt<MODE>(D, row, r0, r1, wb, dump, dump_lo, ktab);
+            else scan_row<J, C2, EX, MODE>(D, row, r0, r1, wb, dump, dump_lo, ktab);
             x += r1 - r0;
         }
     }

@@ -35,7 +35,7 @@ GPUHASH_EHIP = -3
 GPUHASH_ETOOLONG = -4
 GPUHASH_ENOMEM = -5
 GPUHASH_MAX_MSG = 1 << 20
-LAYOUT_AUTO, LAYOUT_UNIFORM, LAYOUT_CLASSIC = 0, 1, 2
+LAYOUT_AUTO, LAYOUT_UNIFORM, LAYOUT_CLASSIC, LAYOUT_LANETABLE = 0, 1, 2, 3
 
 # Every symbol include/gpuhash.h declares (tests check the .so exports all of them).
 EXPORTED = [
@@ -197,7 +197,8 @@ class Engine:
         return self._lib.gpuhash_ndevices(self._ctx)
 
     def set_layout_policy(self, policy: int) -> None:
-        """LAYOUT_AUTO / LAYOUT_UNIFORM / LAYOUT_CLASSIC (gpuhash_set_layout_policy)."""
+        """LAYOUT_AUTO / LAYOUT_UNIFORM / LAYOUT_CLASSIC / LAYOUT_LANETABLE
+        (gpuhash_set_layout_policy)."""
         rc = self._lib.gpuhash_set_layout_policy(self._ctx, policy)
         if rc != GPUHASH_OK:
             raise GpuHashError(rc, "gpuhash_set_layout_policy")

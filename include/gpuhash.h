@@ -112,14 +112,17 @@ int gpuhash_shard_range(size_t msg_len, uint64_t lower, uint64_t upper, int nsha
                         uint64_t *out_lower, uint64_t *out_upper);
 
 /* Layout choice for nonces whose digits straddle two SHA blocks with 5-8 digits in the
- * last one: AUTO (default) takes the uniform-schedule layout when the
- * search fills its lane rows, UNIFORM always takes it, CLASSIC never.  Results are
+ * last one: AUTO (default) takes the uniform-schedule layout (C2 = 2)
+ * when the search fills its lane rows and the lane-table layout (C2 = 3) otherwise;
+ * UNIFORM takes C2 = 2 whenever block B-1 holds >= 3 digits, else C2 = 3; CLASSIC always
+ * the per-nonce-schedule layout (C2 = 1); LANETABLE always C2 = 3.  Results are
  * identical under every policy; only speed differs.  Exposed for tuning and so that
- * parity tests can drive both kernels over small ranges.  Replaces nothing in the
+ * parity tests can drive every kernel over small ranges.  Replaces nothing in the
  * reference. */
 #define GPUHASH_LAYOUT_AUTO 0
 #define GPUHASH_LAYOUT_UNIFORM 1
 #define GPUHASH_LAYOUT_CLASSIC 2
+#define GPUHASH_LAYOUT_LANETABLE 3
 int gpuhash_set_layout_policy(gpuhash_ctx *ctx, int policy);
 
 /* argmin_{n in [lower, upper]} (Hash(msg, n), n) -> *out_hash, *out_nonce.

@@ -91,6 +91,49 @@ def test_uniform_schedule_layouts(engine, oracle, mlen, d, c2, j, request):
         assert engine.min(m, lo, hi) == oracle.min(m, lo, hi), (mlen, d, lo, hi)
 
 
+@pytest.mark.parametrize("mlen,d", [(61, 10), (61, 7), (62, 8), (62, 6), (125, 9), (126, 9)])
+def test_lane_table_layout(engine, oracle, mlen, d):
+    """C2 = 3 (lane table): block B-1 holds 1-2 digits (message lengths =
+    61, 62 mod 64), the lanes take block B's W_0/W_1 digits and keep its schedule in
+    registers, the loop walks the block B-1 values from the host's p-table.  AUTO picks it
+    for these lengths.  Per-nonce parity across loop-value (p-table entry) boundaries and
+    W_0 / W_1 roll-overs, and min parity over whole and partial rectangles."""
+    rng = random.Random(mlen * 100 + d)
+    m = bytes(rng.randrange(32, 127) for _ in range(mlen))
+    nb1 = (mlen + 1) % 64 and 64 - (mlen + 1) % 64
+    RQ = 10 ** (d - nb1)  # lane values per loop value
+    lo_d, hi_d = 10 ** (d - 1), 10 ** d - 1
+    engine.min(m, lo_d, lo_d + 1000)
+    assert {(r["C2"], r["J"]) for r in engine.launches()} == {(3, 1)}, engine.launches()
+    p = rng.randrange(lo_d // RQ + 1, hi_d // RQ)
+    for lo in (p * RQ - 2500, p * RQ + RQ // 2 - 3333, p * RQ + 9_990_000 % RQ - 100):
+        got = engine.hash_range(m, lo, 6000)
+        want = oracle.hash_range(m, lo, 6000)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (mlen, d, lo, int(bad[0]) + lo if bad.size else None)
+    cases = [(p * RQ - 1_000_000, p * RQ + 1_000_000), (p * RQ + 17, p * RQ + 17)]
+    if hi_d - lo_d < 10 ** 6:
+        cases.append((lo_d, hi_d))  # the whole digit group: full rectangles + partial ends
+    for lo, hi in cases:
+        lo, hi = max(lo, lo_d), min(hi, hi_d)
+        assert engine.min(m, lo, hi) == oracle.min(m, lo, hi, threads=8), (mlen, d, lo, hi)
+
+
+def test_lane_table_long_loops_split(engine, oracle, request):
+    """Under LANETABLE a straddle with 5 digits in block B-1 (m = 58, d = 10) loops over
+    up to 10^5 block B-1 values; launches take at most 1024 p-table entries each."""
+    import gpuhash
+    request.addfinalizer(lambda: engine.set_layout_policy(gpuhash.LAYOUT_AUTO))
+    engine.set_layout_policy(gpuhash.LAYOUT_LANETABLE)
+    m = M120[:58]
+    lo, hi = 12345 * 10 ** 5 + 678, (12345 + 1100) * 10 ** 5 + 4321
+    assert engine.min(m, lo, hi) == oracle.min(m, lo, hi, threads=16)
+    assert {(r["C2"], r["J"]) for r in engine.launches()} == {(3, 1)}, engine.launches()
+    got = engine.hash_range(m, (12345 + 1024) * 10 ** 5 - 3000, 6000)
+    want = oracle.hash_range(m, (12345 + 1024) * 10 ** 5 - 3000, 6000)
+    assert (got == want).all()
+
+
 def test_idle_waves_of_partial_rows(engine, oracle, request):
     """A row is 256 lane values (4 waves); a wave whose lanes all lie past the search's
     last lane value skips the row (scan_kernel.h), and in the two-word uniform layout it
@@ -117,12 +160,14 @@ def test_layout_policies_agree(engine, request):
     request.addfinalizer(lambda: engine.set_layout_policy(gpuhash.LAYOUT_AUTO))
     for m, lo, n in ((b"y" * 59, 10 ** 11 + 12345, 3 * 10 ** 10), (M120[:58], 10 ** 9 + 7, 2 * 10 ** 9)):
         got = {}
-        for pol in (gpuhash.LAYOUT_UNIFORM, gpuhash.LAYOUT_CLASSIC, gpuhash.LAYOUT_AUTO):
+        pols = (gpuhash.LAYOUT_UNIFORM, gpuhash.LAYOUT_CLASSIC, gpuhash.LAYOUT_AUTO, gpuhash.LAYOUT_LANETABLE)
+        for pol in pols:
             engine.set_layout_policy(pol)
             got[pol] = engine.min(m, lo, lo + n)
             got[(pol, "c2")] = {r["C2"] for r in engine.launches()}
-        assert got[gpuhash.LAYOUT_UNIFORM] == got[gpuhash.LAYOUT_CLASSIC] == got[gpuhash.LAYOUT_AUTO]
+        assert len({got[pol] for pol in pols}) == 1, got
         assert 2 in got[(gpuhash.LAYOUT_UNIFORM, "c2")] and 2 not in got[(gpuhash.LAYOUT_CLASSIC, "c2")]
+        assert got[(gpuhash.LAYOUT_LANETABLE, "c2")] == {3} and got[(gpuhash.LAYOUT_CLASSIC, "c2")] == {1}
         assert gpuhash.Hash(m, got[gpuhash.LAYOUT_AUTO][1]) == got[gpuhash.LAYOUT_AUTO][0]
     with pytest.raises(gpuhash.GpuHashError):
         engine.set_layout_policy(7)

@@ -45,7 +45,7 @@ def hc():
     return lib
 
 
-AUTO, UNIFORM, CLASSIC = 0, 1, 2
+AUTO, UNIFORM, CLASSIC, LANETABLE = 0, 1, 2, 3
 
 
 def plan(hc, m, a, b, rchunk=0):
@@ -72,6 +72,16 @@ def test_plan_tiles_range_and_layouts_are_legal(hc):
         for x, y in zip(p, p[1:]):
             assert y.lo == x.hi + 1
         for l in p:
+            if l.C2 == 3:  # lane table: lanes = W_0/W_1 digits, loop = block B-1 digits
+                assert l.J == 1 and 5 <= l.q <= 8 and 1 <= l.s <= 8 and not l.EX
+                RQ = 10 ** l.q
+                assert 1 <= l.R <= 1024 and l.r_first == 0 and l.r_last == l.R - 1
+                assert l.lo == l.base + l.p_first and l.hi == l.base + (l.R - 1) * RQ + l.p_last
+                assert l.p_first <= l.p_last < RQ
+                # a rectangle: one loop value, or every lane value of each loop value
+                assert l.R == 1 or (l.p_first == 0 and l.p_last == RQ - 1)
+                assert l.nblocks == (l.p_last - l.p_first) // 256 + 1
+                continue
             if l.C2 == 2:  # two-word uniform loop: W_0 (4 digits) + W_1 (1..4 digits)
                 assert l.J == 1 and 5 <= l.q <= 8 and 3 <= l.s <= 8 and l.s + l.q <= 12
             else:
@@ -84,7 +94,7 @@ def test_plan_tiles_range_and_layouts_are_legal(hc):
             assert l.nrchunks * l.rchunk >= l.R
 
 
-@pytest.mark.parametrize("policy", [AUTO, UNIFORM])
+@pytest.mark.parametrize("policy", [AUTO, UNIFORM, CLASSIC, LANETABLE])
 def test_descriptor_replay_matches_oracle(hc, oracle, policy):
     hc.hostcheck_set_layout_policy(policy)
     rng = random.Random(5)
@@ -101,35 +111,41 @@ def test_descriptor_replay_matches_oracle(hc, oracle, policy):
             for n in {l.lo, l.hi, rng.randrange(l.lo, l.hi + 1)}:
                 assert desc_hash(hc, m, a, b, i, n) == oracle.hash(m, n), (m, a, b, i, n)
     hc.hostcheck_set_layout_policy(AUTO)
-    # every one of the 20 reachable (J, C2, EX) variants was exercised
-    if policy == UNIFORM:
-        assert len(seen) == 20, sorted(seen)
-    else:
-        assert len(seen) >= 19, sorted(seen)
+    # the reachable (J, C2, EX) variants of each policy were all exercised: 14 plain, 3
+    # extra-block, the K+W table (C2 = 1, J = 0), and per policy the J = 1 straddles --
+    # UNIFORM: C2 = 2 and 3; AUTO: C2 = 2 (wide searches) and 3; CLASSIC: C2 = 1 only;
+    # LANETABLE: C2 = 3 only
+    want = {UNIFORM: {(1, 2, 0), (1, 3, 0)}, AUTO: {(1, 2, 0), (1, 3, 0)},
+            CLASSIC: {(1, 1, 0)}, LANETABLE: {(1, 3, 0)}}[policy]
+    straddle = {v for v in seen if v[0] == 1 and v[1] >= 1}
+    assert straddle <= want | {(1, 2, 0)} and want - {(1, 2, 0)} <= straddle, sorted(seen)
+    assert len(seen - straddle) == 18, sorted(seen)
 
 
 def test_layout_policy_for_straddling_j1(hc):
     """m = 59, d = 12: digits 60..71, 4 in block 0 and 8 in block 1 (W_0 + W_1).  The
     uniform two-word loop has R = 10^8 loop values per lane, so AUTO takes it only when
-    its measured partial-row cost model predicts it beats the classic layout; CLASSIC
-    never, UNIFORM always."""
+    its measured partial-row cost model predicts full enough rows, and the lane table
+    (C2 = 3) otherwise; CLASSIC always C2 = 1, LANETABLE always C2 = 3, UNIFORM C2 = 2."""
     m = b"y" * 59
     lo = 10 ** 11
     narrow, wide = (lo, lo + 10 ** 9), (lo, lo + 5 * 10 ** 11)  # both stay at d = 12
     pick = lambda a, b: {(l.J, l.C2) for l in plan(hc, m, a, b)}
-    assert pick(*narrow) == {(1, 1)} and pick(*wide) == {(1, 2)}
+    assert pick(*narrow) == {(1, 3)} and pick(*wide) == {(1, 2)}
     # lane values touched -> the uniform layout's expected rate over the classic one's
     # (profiles/r02_partial_rows.jsonl): one row with 1-4 busy waves, then a full row
     # plus a partial one
     R = 10 ** 8
-    for lanes, c2 in ((45, 1), (64, 2), (100, 1), (128, 2), (160, 1), (192, 2), (215, 2),
+    for lanes, c2 in ((45, 3), (64, 2), (100, 3), (128, 2), (160, 3), (192, 2), (215, 2),
                       (300, 2), (330, 2), (400, 2)):
         assert pick(lo, lo + lanes * R - 1) == {(1, c2)}, lanes
     try:
         hc.hostcheck_set_layout_policy(UNIFORM)
         assert pick(*narrow) == {(1, 2)}
         hc.hostcheck_set_layout_policy(CLASSIC)
-        assert pick(*wide) == {(1, 1)}
+        assert pick(*wide) == {(1, 1)} and pick(*narrow) == {(1, 1)}
+        hc.hostcheck_set_layout_policy(LANETABLE)
+        assert pick(*wide) == {(1, 3)} and pick(*narrow) == {(1, 3)}
     finally:
         hc.hostcheck_set_layout_policy(AUTO)
 
@@ -200,3 +216,26 @@ def test_shards_balance_config4(hc):
     s = shards(hc, 8, 0, (1 << 40) - 1, 8)
     counts = [hi - lo + 1 for lo, hi in s]
     assert max(counts) / min(counts) < 1.03
+
+
+@pytest.mark.parametrize("mlen", [61, 62, 125, 126])
+def test_lane_table_straddles(hc, oracle, mlen):
+    """The layouts C2 = 3 is for: block B-1 holds 1-2 digits (message lengths = 61, 62 mod
+    64, 6-10 digits), with rectangles split at partial first/last loop values, and long
+    loops split at 1024 p-table entries."""
+    m = bytes((i * 29 + 3) % 256 for i in range(mlen))
+    seen = 0
+    for d in range(5, 12):
+        lo, hi = 10 ** (d - 1), 10 ** d - 1
+        rng = random.Random(d * 1000 + mlen)
+        for a, b in [(lo, hi), (lo + 12345, hi - 54321), (rng.randrange(lo, hi), None)]:
+            if b is None:
+                b = min(hi, a + rng.randrange(1, 10 ** 6))
+            p = plan(hc, m, a, b)
+            assert p[0].lo == a and p[-1].hi == b
+            for i, l in enumerate(p):
+                seen += l.C2 == 3
+                pts = {l.lo, l.hi, rng.randrange(l.lo, l.hi + 1)}
+                for n in pts:
+                    assert desc_hash(hc, m, a, b, i, n) == oracle.hash(m, n), (mlen, d, a, b, i, n)
+    assert seen > 0
