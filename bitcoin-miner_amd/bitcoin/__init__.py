@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import json
 import os
+import re
 
 import lsp
 from gpuhash import Hash, Message, MsgType, NewJoin, NewRequest, NewResult
@@ -82,9 +83,15 @@ def _u64(d: dict, key: str) -> int:
     return v
 
 
+_LONE_SURROGATE = re.compile("[\ud800-\udfff]")
+
+
 def unmarshal(raw: bytes) -> Message:
     """json.Unmarshal into bitcoin.Message (message.go:16-21); raises ValueError where Go
     would return an error, so callers drop the message as the reference would."""
+    if isinstance(raw, (bytes, bytearray)):
+        # Go's decoder turns invalid UTF-8 into U+FFFD instead of failing the message
+        raw = bytes(raw).decode("utf-8", "replace")
     d = json.loads(raw)
     if not isinstance(d, dict):
         raise ValueError("json: cannot unmarshal non-object into Go value of type bitcoin.Message")
@@ -96,6 +103,9 @@ def unmarshal(raw: bytes) -> Message:
         data = ""
     if not isinstance(data, str):
         raise ValueError(f"json: cannot unmarshal {type(data).__name__} into Go struct field Message.Data of type string")
+    # a "\ud800" escape without its pair: Go decodes it to U+FFFD (json.loads keeps the lone
+    # surrogate, which has no UTF-8 bytes to hash); valid pairs are already combined
+    data = _LONE_SURROGATE.sub("\ufffd", data)
     return Message(MsgType(t), Data=data, Lower=_u64(d, "Lower"), Upper=_u64(d, "Upper"),
                    Hash=_u64(d, "Hash"), Nonce=_u64(d, "Nonce"))
 

@@ -134,43 +134,37 @@ GroupLayout layout_for(uint64_t m, int d, uint64_t span = 0, int policy = kLayou
     // digit bytes of block B that precede word J
     uint64_t nbB = (f_abs >= wstart) ? 0 : wstart - std::max(f_abs, blkB);
     g.C2 = (uint64_t)g.s > nbB;
-    // J = 1 with lanes spilling into block B-1: W_0 is four digits.  When block B-1 holds
-    // at least 3 digits (>= 1000 lane values, rows stay full), move W_0's digits into the
-    // loop so block B carries loop digits only (C2 = 2: uniform schedule, no per-nonce
-    // schedule work); the lanes take the digits at the end of block B-1.
-    // A lane then covers R = 10^(4+q1) loop values, up to 10^8, so a narrow search fills
-    // only part of a 256-lane row.  A wave with no lane skips the row (scan_kernel.h), but
-    // a partial row still costs more than its share of waves: measured row times, as a
-    // fraction of a full row's, for 1-4 busy waves (a wave with any lane is busy) are
-    // 0.30 / 0.58 / 0.975 / 1 when the search is that one row, and 0.33 / 0.77 / 0.98 / 1
-    // for the last row after full ones (profiles/r02_partial_rows.jsonl).  Keep the
-    // classic layout (31.7 GH/s) unless the uniform one (45.6 GH/s on full rows) is
-    // expected to be faster: lanes / (256 * row cost) >= 31.7 / 45.6 ~ 0.70.
+    // J = 1 with lanes spilling into block B-1: W_0 is four digits, W_1 holds q digits.
+    // Three layouts can run such a digit group:
+    //   C2 = 1 (classic)    lanes in W_0 + block B-1, W_1 per nonce: every nonce pays
+    //                       block B's schedule, ~31.7 GH/s;
+    //   C2 = 2 (two-word)   lanes = block B-1 digits, the loop takes W_0 and W_1: block B's
+    //                       schedule is wave-uniform (built in LDS per 64 loop values),
+    //                       45.2-45.7 GH/s on full 256-lane rows, but a lane covers up to
+    //                       10^8 loop values, so narrow searches leave rows partly empty;
+    //   C2 = 3 (lane table) lanes = the W_0/W_1 digits (>= 10^5 values: rows always fill),
+    //                       each lane keeps block B's schedule in registers, the loop runs
+    //                       over the block B-1 values whose chaining values the host
+    //                       precomputes: 44-46.3 GH/s, >= C2 = 2 on every measured layout,
+    //                       full rows included (profiles/r03_sweep_lt_vs_u2.jsonl).
+    // AUTO takes C2 = 3 unless the search touches more than kMaxLtTable block B-1 values
+    // (its host table: 64 B and one host compression per value), where C2 = 2 rows are
+    // full anyway.  UNIFORM keeps the round-2 rule (C2 = 2 whenever block B-1 holds >= 3
+    // digits), CLASSIC and LANETABLE force their layout (tuning and parity tests).
     if (g.C2 && g.J == 1) {
         const int nb1 = d - 4 - g.q;  // digits in block B-1 and earlier
-        bool fill_ok = policy != kLayoutClassic;
-        if (span && policy == kLayoutAuto) {
-            static constexpr double kOneRow[5] = {0.0, 0.30, 0.58, 0.975, 1.0};
-            static constexpr double kLastRow[5] = {0.0, 0.33, 0.77, 0.98, 1.0};
-            const uint64_t lanes = (span - 1) / pow10u(4 + g.q) + 1;  // lane values touched
-            const uint64_t full = lanes / kBlock, rem = lanes % kBlock;
-            const uint64_t busy = (rem + 63) / 64;  // busy waves of the partial row
-            const double cost = (double)full + (full ? kLastRow[busy] : kOneRow[busy]);
-            fill_ok = (double)lanes / (kBlock * cost) >= 0.70;
-        }
-        if (policy == kLayoutLaneTable) fill_ok = false;
-        if (nb1 >= 3 && fill_ok) {
+        const uint64_t RQ = pow10u(4 + g.q);
+        const uint64_t nloop = span ? (span - 1) / RQ + 2 : pow10u(std::min(nb1, 6));
+        int c2 = 3;
+        if (policy == kLayoutClassic) c2 = 1;
+        else if (policy == kLayoutUniform) c2 = nb1 >= 3 ? 2 : 3;
+        else if (policy == kLayoutAuto) c2 = (nb1 >= 3 && nloop > kMaxLtTable) ? 2 : 3;
+        if (c2 == 2) {
             g.C2 = 2;
             g.q1 = g.q;
             g.q = 4 + g.q;
             g.s = std::min(std::min(kMaxLane, nb1), kMaxLaunchDigitsU2 - g.q);
-        } else if (policy != kLayoutClassic) {
-            // C2 = 3 (lane table): block B still carries loop-free digits only, but the
-            // LANES take its 4 + q1 digits (>= 10^5 values: rows always fill) and keep its
-            // schedule in registers, while the loop runs over the few block B-1 values
-            // the rows of C2 = 2 could not fill (1-2 digits, or a narrow search).  A nonce
-            // then costs block B's 64 rounds, as in C2 = 2, against a full per-nonce
-            // schedule in the classic layout.
+        } else if (c2 == 3) {
             g.C2 = 3;
             g.q1 = g.q;
             g.q = 4 + g.q;

@@ -93,14 +93,16 @@ static constexpr int kMaxLaunchDigits = 10;   // s + q <= 10  -> <= 10^10 nonces
 static constexpr int kMaxLaunchDigitsU2 = 12;
 
 // Choice between the J = 1 straddling layouts (plan.cpp layout_for):
-//   auto       C2 = 2 (uniform two-word loop) when its measured partial-row cost model
-//              predicts full enough rows, else C2 = 3 (lane table)
+//   auto       C2 = 3 (lane table), or C2 = 2 (uniform two-word loop) when the search
+//              touches more than kMaxLtTable block B-1 values
 //   uniform    C2 = 2 whenever block B-1 holds >= 3 digits, else C2 = 3 (tuning / tests)
 //   classic    C2 = 1: lanes in W_0 and block B-1, per-nonce schedule (tuning / tests)
 //   lanetable  C2 = 3 always (tuning / tests)
 enum LayoutPolicy { kLayoutAuto = 0, kLayoutUniform = 1, kLayoutClassic = 2, kLayoutLaneTable = 3 };
-// C2 = 3: at most this many loop values (p-table entries) per launch
+// C2 = 3: at most this many loop values (p-table entries) per launch, and AUTO takes the
+// layout only for searches touching at most kMaxLtTable block B-1 values (4 MB of table)
 static constexpr uint32_t kMaxLtLoop = 1024;
+static constexpr uint64_t kMaxLtTable = 65536;
 
 // Plans [lower, upper] (inclusive, lower <= upper) of `msg`.  `rchunk_max` caps the r
 // values per work item (0 = default).  Appends to `out`.

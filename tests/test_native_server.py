@@ -258,3 +258,33 @@ def test_a_small_request_is_not_starved_by_a_large_one(procs, plain_server, mine
     big._loop.stop()  # leave without waiting: the server drops the large request
     time.sleep(P.EpochLimit * P.EpochMillis / 1000 + 0.5)
     assert "dropped request" in s.log()
+
+
+def _longest_servable_data():
+    """Largest ASCII Data whose worst-case job frame still fits one LSP datagram."""
+    import lspnet
+    from bitcoin.server import job_frame_worst_case
+    n = 1000
+    while len(job_frame_worst_case("d" * (n + 1))) <= lspnet.MAX_DATAGRAM:
+        n += 1
+    return n
+
+
+def test_jobs_must_fit_one_datagram_python_and_compiled(procs, plain_server, miner_bin, oracle):
+    """a request that fits a datagram can yield jobs that do not (20-digit
+    job bounds where the client sent Lower = 0); such a job would be truncated and
+    resent forever.  Both servers refuse the request at the same length, and serve the
+    longest one whose jobs fit, end to end."""
+    import lspnet
+    from bitcoin.server import request_error
+    n = _longest_servable_data()
+    client_frame = lsp.message.NewData(1, 1, bitcoin.marshal(bitcoin.NewRequest("d" * (n + 1), 0, 99))).marshal()
+    assert len(client_frame) <= lspnet.MAX_DATAGRAM  # the client's own Request fits
+    assert request_error("d" * n, 0, 99) is None
+    assert "datagram" in request_error("d" * (n + 1), 0, 99)
+    s = System(procs, plain_server, miner_bin, GPUHASH_JOB_SIZE=40)
+    s.miner()
+    assert s.request("d" * (n + 1), 99) is None  # Disconnected
+    assert s.request("d" * n, 99) == oracle.min(b"d" * n, 0, 99)
+    log = s.log()
+    assert "would not fit a 2000-byte LSP datagram" in log, log

@@ -113,9 +113,10 @@ def test_descriptor_replay_matches_oracle(hc, oracle, policy):
     hc.hostcheck_set_layout_policy(AUTO)
     # the reachable (J, C2, EX) variants of each policy were all exercised: 14 plain, 3
     # extra-block, the K+W table (C2 = 1, J = 0), and per policy the J = 1 straddles --
-    # UNIFORM: C2 = 2 and 3; AUTO: C2 = 2 (wide searches) and 3; CLASSIC: C2 = 1 only;
+    # UNIFORM: C2 = 2 and 3; AUTO: C2 = 3 (and 2 on searches of > 65536 block B-1 values,
+    # which this test's ranges rarely reach); CLASSIC: C2 = 1 only;
     # LANETABLE: C2 = 3 only
-    want = {UNIFORM: {(1, 2, 0), (1, 3, 0)}, AUTO: {(1, 2, 0), (1, 3, 0)},
+    want = {UNIFORM: {(1, 2, 0), (1, 3, 0)}, AUTO: {(1, 3, 0)},
             CLASSIC: {(1, 1, 0)}, LANETABLE: {(1, 3, 0)}}[policy]
     straddle = {v for v in seen if v[0] == 1 and v[1] >= 1}
     assert straddle <= want | {(1, 2, 0)} and want - {(1, 2, 0)} <= straddle, sorted(seen)
@@ -123,29 +124,29 @@ def test_descriptor_replay_matches_oracle(hc, oracle, policy):
 
 
 def test_layout_policy_for_straddling_j1(hc):
-    """m = 59, d = 12: digits 60..71, 4 in block 0 and 8 in block 1 (W_0 + W_1).  The
-    uniform two-word loop has R = 10^8 loop values per lane, so AUTO takes it only when
-    its measured partial-row cost model predicts full enough rows, and the lane table
-    (C2 = 3) otherwise; CLASSIC always C2 = 1, LANETABLE always C2 = 3, UNIFORM C2 = 2."""
+    """J = 1 straddles (4 + q1 digits in block B's W_0/W_1, the rest in block B-1).  AUTO
+    takes the lane table (C2 = 3) unless the search touches more than 65536 block B-1
+    values, then the two-word uniform loop (C2 = 2), whose rows are full there; CLASSIC
+    always C2 = 1, LANETABLE always C2 = 3, UNIFORM C2 = 2 whenever block B-1 holds >= 3
+    digits (round 2's rule)."""
+    pick = lambda m, a, b: {(l.J, l.C2) for l in plan(hc, m, a, b)}
+    # m = 59, d = 12: 4 digits in block 0, 8 in block 1 (RQ = 10^8): at most 9000 values
     m = b"y" * 59
     lo = 10 ** 11
-    narrow, wide = (lo, lo + 10 ** 9), (lo, lo + 5 * 10 ** 11)  # both stay at d = 12
-    pick = lambda a, b: {(l.J, l.C2) for l in plan(hc, m, a, b)}
-    assert pick(*narrow) == {(1, 3)} and pick(*wide) == {(1, 2)}
-    # lane values touched -> the uniform layout's expected rate over the classic one's
-    # (profiles/r02_partial_rows.jsonl): one row with 1-4 busy waves, then a full row
-    # plus a partial one
-    R = 10 ** 8
-    for lanes, c2 in ((45, 3), (64, 2), (100, 3), (128, 2), (160, 3), (192, 2), (215, 2),
-                      (300, 2), (330, 2), (400, 2)):
-        assert pick(lo, lo + lanes * R - 1) == {(1, c2)}, lanes
+    narrow, wide = (lo, lo + 10 ** 9), (lo, lo + 5 * 10 ** 11)
+    assert pick(m, *narrow) == {(1, 3)} and pick(m, *wide) == {(1, 3)}
+    # m = 56, d = 12: 7 digits in block 0, 5 in block 1 (RQ = 10^5)
+    m56 = b"z" * 56
+    assert pick(m56, lo, lo + 65000 * 10 ** 5) == {(1, 3)}
+    assert pick(m56, lo, lo + 70000 * 10 ** 5) == {(1, 2)}
     try:
         hc.hostcheck_set_layout_policy(UNIFORM)
-        assert pick(*narrow) == {(1, 2)}
+        assert pick(m, *narrow) == {(1, 2)}
+        assert pick(b"q" * 61, 10 ** 9, 10 ** 9 + 10 ** 7) == {(1, 3)}  # 2 digits in block 0
         hc.hostcheck_set_layout_policy(CLASSIC)
-        assert pick(*wide) == {(1, 1)} and pick(*narrow) == {(1, 1)}
+        assert pick(m, *wide) == {(1, 1)} and pick(m, *narrow) == {(1, 1)}
         hc.hostcheck_set_layout_policy(LANETABLE)
-        assert pick(*wide) == {(1, 3)} and pick(*narrow) == {(1, 3)}
+        assert pick(m, *wide) == {(1, 3)} and pick(m56, lo, lo + 70000 * 10 ** 5) == {(1, 3)}
     finally:
         hc.hostcheck_set_layout_policy(AUTO)
 

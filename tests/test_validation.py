@@ -85,11 +85,15 @@ def test_scheduler_rejects_unservable_ranges(lo, hi):
     assert s.next_assignment() is None  # nothing was cut
 
 
-def test_scheduler_rejects_data_over_engine_cap():
+def test_scheduler_rejects_data_over_engine_cap_and_datagram():
     s = bserver.Scheduler(job_size=10)
-    with pytest.raises(ValueError):
+    with pytest.raises(ValueError, match="engine"):
         s.add_request(client=100, data="a" * (gpuhash.GPUHASH_MAX_MSG + 1), lower=0, upper=9)
-    s.add_request(client=100, data="a" * gpuhash.GPUHASH_MAX_MSG, lower=0, upper=9)
+    # the LSP datagram (2000 bytes, lspnet/conn.go:35) is the tighter cap: the job frames
+    # must fit it (tests/test_native_server.py finds the exact boundary for both servers)
+    with pytest.raises(ValueError, match="datagram"):
+        s.add_request(client=100, data="a" * 1400, lower=0, upper=9)
+    s.add_request(client=100, data="a" * 1300, lower=0, upper=9)
 
 
 def test_scheduler_accepts_full_u64_and_single_nonce():
@@ -357,3 +361,15 @@ def test_marshal_is_byte_exact_with_go(msg, raw):
 
 def test_marshal_replaces_invalid_utf8_like_go():
     assert bitcoin.marshal(bitcoin.NewRequest("x\ud800y", 1, 2)).startswith(b'{"Type":1,"Data":"x\xef\xbf\xbdy"')
+
+
+def test_unmarshal_replaces_lone_surrogates_and_bad_utf8_like_go():
+    """Go's json.Unmarshal decodes a lone surrogate escape and invalid UTF-8
+    to U+FFFD (so the message is served, and hashed as EF BF BD), as lsp_native.h does;
+    the Python side used to keep the lone surrogate and then fail the request."""
+    m = bitcoin.unmarshal(b'{"Type":1,"Data":"a\\ud800b\\udc00c","Lower":0,"Upper":5}')
+    assert m.Data == "a�b�c"
+    assert bitcoin.unmarshal(b'{"Type":1,"Data":"\\ud83d\\ude00","Lower":0,"Upper":5}').Data == "\U0001F600"
+    assert bitcoin.unmarshal(b'{"Type":1,"Data":"x\xff\xfey","Lower":0,"Upper":5}').Data == "x��y"
+    assert bserver.request_error(m.Data, 0, 5) is None
+    assert m.Data.encode() == b"a\xef\xbf\xbdb\xef\xbf\xbdc"

@@ -37,10 +37,9 @@ for step in "$@"; do
         systest) run pytest_sys 600 python -u -m pytest tests/test_gpu_system.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 300 python -u bench.py --steps 10 --warmup 2 ;;
-        nccl1) run nccl1 300 env GPUHASH_FORCE_DIST=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29541 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
-        dist2) run dist2 300 env GPUHASH_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 ;;
-        inproc) run inproc1 300 python -u bench.py --inproc 0 --steps 5 --warmup 1
-                run inproc2 300 python -u bench.py --inproc 0,0 --steps 3 --warmup 1 ;;
+        nccl1) run nccl1 300 env GPUHASH_FORCE_DIST=1 GPUHASH_DIST_BACKEND=nccl python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29541 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
+        dist2) run dist2 300 env GPUHASH_SHARE_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 ;;
+        inproc) run inproc2 300 python -u bench.py --inproc 0,0 --steps 3 --warmup 1 --no-cpu-baseline ;;
         latency) run latency 120 python -u tools/latency.py ;;
         ranks) run ranks 300 python -u tools/rank_windows.py --ranks "${RANKS:-0,1,2,3,4,5,6,7}" ;;
         sweep) run sweep 600 python -u tools/layout_sweep.py ;;
@@ -54,7 +53,7 @@ for step in "$@"; do
                run sys5an 900 python -u tools/system_bench.py --adaptive --native ;;
         soak) run soak 400 python -u tools/soak.py "${SOAK_SECONDS:-90}" "${SOAK_SEED:-2026}" ;;
         c4full) run c4full 400 python -u tools/config4_full.py ;;
-        dist8c4) run dist8c4 400 env GPUHASH_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29547 bench.py --gpus 8 --config 4 --steps 1 --warmup 0 ;;
+        dist8c4) run dist8c4 400 env GPUHASH_SHARE_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29547 bench.py --gpus 8 --config 4 --steps 1 --warmup 0 ;;
         bench3) run bench3 300 python -u bench.py --config 3 --steps 5 --warmup 1 ;;
         bench4) run bench4 300 python -u bench.py --config 4 --steps 2 --warmup 1 ;;
         prof4) run prof_c4 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c4" -o bench --output-format csv -- python3 bench.py --config 4 --steps 1 --warmup 1 --no-cpu-baseline ;;

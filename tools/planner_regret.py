@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Does the planner's AUTO layout choice ever lose to a forced one?  For the message
 lengths whose nonce digits straddle a block boundary (where AUTO chooses between the
-two-word uniform layout and the classic one, plan.cpp), several digit counts and search
-widths, time the same search under AUTO, UNIFORM and CLASSIC and report AUTO's rate over
+two-word uniform layout, the lane table and the classic one, plan.cpp), several digit
+counts and search widths, time the same search under AUTO and every forced policy
+(UNIFORM, CLASSIC, LANETABLE) and report AUTO's rate over
 the best forced one (1.0 = AUTO picked the faster layout).  Answers must agree.
 
   python tools/planner_regret.py [--lens 54,...] [--digits 10,11,12] [--bits 26,29,32]
@@ -25,7 +26,8 @@ def main() -> None:
     args = ap.parse_args()
     import gpuhash
     eng = gpuhash.Engine([0])
-    pols = {"auto": gpuhash.LAYOUT_AUTO, "uniform": gpuhash.LAYOUT_UNIFORM, "classic": gpuhash.LAYOUT_CLASSIC}
+    pols = {"auto": gpuhash.LAYOUT_AUTO, "uniform": gpuhash.LAYOUT_UNIFORM, "classic": gpuhash.LAYOUT_CLASSIC,
+            "lanetable": gpuhash.LAYOUT_LANETABLE}
     worst = 1e9
     for m in [int(x) for x in args.lens.split(",")]:
         msg = bytes((i * 37 + 11) % 94 + 32 for i in range(m))
@@ -48,7 +50,7 @@ def main() -> None:
                     if name == "auto":
                         row["auto_C2"] = sorted({x["C2"] for x in eng.launches()})
                 row["same"] = len(res) == 1
-                row["auto_over_best"] = round(row["auto"] / max(row["uniform"], row["classic"]), 3)
+                row["auto_over_best"] = round(row["auto"] / max(row[k] for k in pols if k != "auto"), 3)
                 worst = min(worst, row["auto_over_best"])
                 print(json.dumps(row), flush=True)
     eng.set_layout_policy(gpuhash.LAYOUT_AUTO)
