@@ -222,7 +222,7 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
         bytes += sizeof(LaunchDesc) * groups[g].idx.size();
         bytes = (bytes + 15) & ~(size_t)15;
         ptab_at[g] = bytes;
-        for (size_t k : groups[g].idx) bytes += sizeof(uint32_t) * plan[k].ptab.size();
+        for (size_t k : groups[g].idx) bytes += sizeof(uint32_t) * plan[k].nptab;
         bytes = (bytes + 15) & ~(size_t)15;
     }
     int rc = dev_reserve_meta(d, bytes);
@@ -238,7 +238,6 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
     for (size_t g = 0; g < groups.size(); g++) {
         auto* offs = reinterpret_cast<unsigned long long*>(d.h_meta + offs_at[g]);
         auto* descs = reinterpret_cast<LaunchDesc*>(d.h_meta + desc_at[g]);
-        auto* ptabs = reinterpret_cast<uint32_t*>(d.h_meta + ptab_at[g]);
         uint32_t ptab_words = 0;
         unsigned long long acc = 0;
         for (size_t k = 0; k < groups[g].idx.size(); k++) {
@@ -247,10 +246,9 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
             offs[k] = acc;
             acc += (unsigned long long)((D.p_last - D.p_first) / (uint32_t)kBlock + 1u) * D.R;
             descs[k] = D;
-            if (l.C2 == 3) {  // lane table: this launch's p-table, after the group's descs
-                std::memcpy(ptabs + ptab_words, l.ptab.data(), sizeof(uint32_t) * l.ptab.size());
+            if (l.C2 == 3) {  // lane table: room for this launch's p-table (k_ptab fills it)
                 descs[k].tab_off = ptab_words;
-                ptab_words += (uint32_t)l.ptab.size();
+                ptab_words += l.nptab;
             }
             if (l.C2 == 1 && l.J == 0) {
                 auto it = std::find_if(tabs.begin(), tabs.end(), [&](const Tab& t) { return t.d == l.d; });
@@ -280,6 +278,14 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
     for (const Tab& t : tabs)
         HIPCHK(launch_ktab(reinterpret_cast<const LaunchDesc*>(d.d_meta + t.desc_byte), d.d_ktab + t.off,
                            t.R, d.stream));
+    // lane-table groups: their launches' p-tables, one device thread per block B-1 value
+    // (on the host these compressions cost ~0.16 us each, ~7% of a search whose loop
+    // values cover only 10^5 lane values each)
+    for (size_t g = 0; g < groups.size(); g++)
+        if (groups[g].C2 == 3)
+            HIPCHK(launch_ptab(reinterpret_cast<const LaunchDesc*>(d.d_meta + desc_at[g]),
+                               (int)groups[g].idx.size(), reinterpret_cast<uint32_t*>(d.d_meta + ptab_at[g]),
+                               d.stream));
     HIPCHK(hipMemsetAsync(d.d_thresh, 0xFF, sizeof(unsigned long long), d.stream));
     HIPCHK(hipMemsetAsync(d.d_best, 0xFF, sizeof(Cand), d.stream));
     HIPCHK(hipMemsetAsync(d.d_ncand, 0, sizeof(unsigned int), d.stream));

@@ -78,7 +78,7 @@ int gpuhash_shard(uint64_t msg_len, uint64_t lower, uint64_t upper, int n, uint6
 int hostcheck_desc_hash(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper,
                         uint32_t rchunk, int idx, uint64_t nonce, uint64_t* out) {
     std::vector<Launch> v;
-    plan_range(msg, len, lower, upper, v, rchunk, g_policy);
+    plan_range(msg, len, lower, upper, v, rchunk, g_policy, /*host_ptab=*/true);
     if (idx < 0 || idx >= (int)v.size()) return -1;
     const Launch& l = v[(size_t)idx];
     const LaunchDesc& D = l.desc;

@@ -38,6 +38,10 @@ hipError_t launch_scan(int J, int C2, int EX, int mode, const ScanArgs& a);
 // Fills the uniform K+W table of a C2/J=0 descriptor: tab[64*r + t] = K[t] + W_t(r),
 // r in [0, D.R), for block B's words U with the loop digits of r inserted into W_0.
 hipError_t launch_ktab(const LaunchDesc* d_desc, uint32_t* tab, uint32_t R, hipStream_t stream);
+// Fills the p-tables of ndesc lane-table (C2 = 3) descriptors: for descriptor i and k < R,
+// tab[desc.tab_off + 16k ...] = block B-1's chaining value for p = lt_p0 + k, then round 0's
+// partial sums inv0, t20 of block B (scan_row_lt).
+hipError_t launch_ptab(const LaunchDesc* d_descs, int ndesc, uint32_t* tab, hipStream_t stream);
 hipError_t launch_reduce(Cand* cands, unsigned int* ncand, Cand* best, hipStream_t stream);
 
 }  // namespace gpuhash

@@ -145,6 +145,13 @@ hipError_t launch_ktab(const LaunchDesc* d_desc, uint32_t* tab, uint32_t R, hipS
     return hipGetLastError();
 }
 
+hipError_t launch_ptab(const LaunchDesc* d_descs, int ndesc, uint32_t* tab, hipStream_t stream) {
+    if (!d_descs || !tab || ndesc <= 0) return hipErrorInvalidValue;
+    // kMaxLtLoop = 1024 loop values per descriptor: 4 workgroups of 256 per descriptor
+    hipLaunchKernelGGL(k_ptab, dim3(kMaxLtLoop / 256u, (unsigned)ndesc), dim3(256), 0, stream, d_descs, tab);
+    return hipGetLastError();
+}
+
 hipError_t launch_reduce(Cand* cands, unsigned int* ncand, Cand* best, hipStream_t stream) {
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, stream, cands, ncand, best);
     return hipGetLastError();

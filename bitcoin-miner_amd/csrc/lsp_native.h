@@ -2,7 +2,12 @@
 // (miner_main.cpp, server_main.cpp).  Header-only; no HIP, no gpuhash types.
 //
 //   * JSON as Go's encoding/json reads and writes the two message types: lsp.Message
-//     (lsp/message.go:17-22) and bitcoin.Message (bitcoin/message.go:16-21);
+//     (lsp/message.go:17-22) and bitcoin.Message (bitcoin/message.go:16-21).  Known
+//     divergences of the reader from json.Unmarshal, both on input the reference's own
+//     programs never write: an unknown key whose value is an object or array fails the
+//     whole message (Go skips unknown fields of any shape), and keys match
+//     case-sensitively (Go also accepts "type" for "Type").  Such a message is dropped, as
+//     Go drops a message it cannot decode;
 //   * lspnet's UDP endpoints with per-role drop injection (lspnet/conn.go:34-113,
 //     staff.go:14-58), the percentages taken from LSPNET_{CLIENT,SERVER}_{READ,WRITE}_DROP
 //     like the Python programs;

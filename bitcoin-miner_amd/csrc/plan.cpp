@@ -148,8 +148,8 @@ GroupLayout layout_for(uint64_t m, int d, uint64_t span = 0, int policy = kLayou
     //                       precomputes: 44-46.3 GH/s, >= C2 = 2 on every measured layout,
     //                       full rows included (profiles/r03_sweep_lt_vs_u2.jsonl).
     // AUTO takes C2 = 3 unless the search touches more than kMaxLtTable block B-1 values
-    // (its host table: 64 B and one host compression per value), where C2 = 2 rows are
-    // full anyway.  UNIFORM keeps the round-2 rule (C2 = 2 whenever block B-1 holds >= 3
+    // (its table: 64 B and one compression per value), where C2 = 2 rows are full anyway,
+    // or fewer than ~2 (a row's schedule build would not amortise): C2 = 1 there.  UNIFORM keeps the round-2 rule (C2 = 2 whenever block B-1 holds >= 3
     // digits), CLASSIC and LANETABLE force their layout (tuning and parity tests).
     if (g.C2 && g.J == 1) {
         const int nb1 = d - 4 - g.q;  // digits in block B-1 and earlier
@@ -158,7 +158,14 @@ GroupLayout layout_for(uint64_t m, int d, uint64_t span = 0, int policy = kLayou
         int c2 = 3;
         if (policy == kLayoutClassic) c2 = 1;
         else if (policy == kLayoutUniform) c2 = nb1 >= 3 ? 2 : 3;
-        else if (policy == kLayoutAuto) c2 = (nb1 >= 3 && nloop > kMaxLtTable) ? 2 : 3;
+        else if (policy == kLayoutAuto) {
+            // a row of the lane table builds block B's schedule once (~550 VALU) for every
+            // loop value it then hashes: below ~2 loop values the classic layout's
+            // per-nonce schedule (~1,300 VALU per nonce) is cheaper
+            // (profiles/r03_planner_regret.jsonl: 26.2 vs 29.0 GH/s at 0.7 loop values)
+            if (span && span < 2 * RQ) c2 = 1;
+            else c2 = (nb1 >= 3 && nloop > kMaxLtTable) ? 2 : 3;
+        }
         if (c2 == 2) {
             g.C2 = 2;
             g.q1 = g.q;
@@ -200,7 +207,7 @@ Prefix make_prefix(const uint8_t* msg, uint64_t m) {
 }
 
 void build_launch(const uint8_t* msg, uint64_t m, const Prefix& pre, const GroupLayout& g, uint64_t H,
-                  uint64_t lo, uint64_t hi, uint32_t rchunk_max, Launch& out) {
+                  uint64_t lo, uint64_t hi, uint32_t rchunk_max, Launch& out, bool host_ptab) {
     const int d = g.d, q = g.q, s = g.s, h = d - s - q;
     const uint64_t L = m + 1 + (uint64_t)d;
     const uint64_t nblk = g.B + 1 + (uint64_t)g.EX;
@@ -278,12 +285,16 @@ void build_launch(const uint8_t* msg, uint64_t m, const Prefix& pre, const Group
         D.r_first = 0;
         D.r_last = NP - 1u;
         D.base = H * U + p_a * RQ;
+        D.lt_p0 = (uint32_t)p_a;
+        out.nptab = 16u * NP;
         // p-table: block B-1 with the s loop digits of p (its last s bytes), compressed
-        // from CV1, then round 0 of block B up to its K+W term
-        out.ptab.assign(16ull * NP, 0u);
+        // from CV1, then round 0 of block B up to its K+W term.  The library builds it on
+        // the device (k_ptab, the same steps); the host copy is for the CPU replay.
+        out.ptab.clear();
+        if (host_ptab) out.ptab.assign(16ull * NP, 0u);
         std::vector<uint8_t> blk(64);
         std::memcpy(blk.data(), &buf[(g.B - 1 - p0) * 64], 64);
-        for (uint32_t k = 0; k < NP; k++) {
+        for (uint32_t k = 0; host_ptab && k < NP; k++) {
             uint64_t v = p_a + k;
             for (int i = s - 1; i >= 0; i--) { blk[64 - (size_t)s + (size_t)i] = (uint8_t)('0' + v % 10u); v /= 10u; }
             uint32_t w[16], cv[8];
@@ -304,6 +315,7 @@ void build_launch(const uint8_t* msg, uint64_t m, const Prefix& pre, const Group
         return;
     }
     out.ptab.clear();
+    out.nptab = 0;
     const uint64_t R = pow10u(q), P = pow10u(s);
     D.R = (uint32_t)R;
     // r values per work item: ~100 keeps every workgroup short (a few ms at full load)
@@ -329,7 +341,7 @@ void build_launch(const uint8_t* msg, uint64_t m, const Prefix& pre, const Group
 }  // namespace
 
 void plan_range(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper,
-                std::vector<Launch>& out, uint32_t rchunk_max, int policy) {
+                std::vector<Launch>& out, uint32_t rchunk_max, int policy, bool host_ptab) {
     const int dlo = num_digits(lower), dhi = num_digits(upper);
     const Prefix pre = make_prefix(msg, len);
     for (int d = dlo; d <= dhi; d++) {
@@ -363,13 +375,13 @@ void plan_range(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper
                         end = pe * RQ + RQ - 1;
                     }
                     Launch l;
-                    build_launch(msg, len, pre, g, H, base + o, base + end, rchunk_max, l);
+                    build_launch(msg, len, pre, g, H, base + o, base + end, rchunk_max, l, host_ptab);
                     out.push_back(std::move(l));
                     o = end + 1;
                 }
             } else {
                 Launch l;
-                build_launch(msg, len, pre, g, H, lo, hi, rchunk_max, l);
+                build_launch(msg, len, pre, g, H, lo, hi, rchunk_max, l, host_ptab);
                 out.push_back(std::move(l));
             }
             if (H == Hl) break;

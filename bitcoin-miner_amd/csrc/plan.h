@@ -71,6 +71,8 @@ struct LaunchDesc {
     uint32_t R1;       // C2 = 2, 3: 10^(digits of W_1); (W_0, W_1) digits = (x / R1, x % R1)
     uint32_t RQ;       // C2 = 3: 10^q, lane values per loop value
     uint64_t base;     // nonce = base + p·R + r  (C2 = 3: base + r·RQ + p, p = lane value)
+    uint32_t lt_p0;    // C2 = 3: block B-1 value of loop value 0 (p-table entry k: lt_p0 + k)
+    uint32_t pad2_;
 };
 
 struct Launch {
@@ -82,7 +84,10 @@ struct Launch {
     uint64_t lo, hi;      // inclusive nonce range covered
     uint32_t nblocks;     // grid size (workgroups of 256)
     LaunchDesc desc;
-    std::vector<uint32_t> ptab;  // C2 = 3: 16 words per loop value (LaunchDesc::tab_off)
+    uint32_t nptab = 0;          // C2 = 3: p-table words (16 per loop value, LaunchDesc::tab_off)
+    std::vector<uint32_t> ptab;  // C2 = 3: the p-table, filled on the host only when planned
+                                 //   with host_ptab (the CPU replay); the library builds it
+                                 //   on the device (k_ptab)
 };
 
 // Largest number of lane digits; 10^kMaxLane lanes per launch.
@@ -107,7 +112,8 @@ static constexpr uint64_t kMaxLtTable = 65536;
 // Plans [lower, upper] (inclusive, lower <= upper) of `msg`.  `rchunk_max` caps the r
 // values per work item (0 = default).  Appends to `out`.
 void plan_range(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper,
-                std::vector<Launch>& out, uint32_t rchunk_max = 0, int policy = kLayoutAuto);
+                std::vector<Launch>& out, uint32_t rchunk_max = 0, int policy = kLayoutAuto,
+                bool host_ptab = false);
 
 struct Shard {
     uint64_t lo, hi;  // inclusive

@@ -25,6 +25,7 @@ __global__ void k_scan(const LaunchDesc* __restrict__ descs, const unsigned long
                        const uint32_t* __restrict__ ktab);
 
 __global__ void k_ktab(const LaunchDesc* __restrict__ desc, uint32_t* __restrict__ tab, uint32_t R);
+__global__ void k_ptab(const LaunchDesc* __restrict__ descs, uint32_t* __restrict__ tab);
 
 }  // namespace gpuhash
 

@@ -428,6 +428,9 @@ __device__ __forceinline__ void scan_row_lt(const LaunchDesc& D, uint32_t row, u
     }
 #pragma unroll 1
     for (uint32_t r = r0; r < r1; r++) {
+#ifdef GPUHASH_LT_ALIGN
+        GPUHASH_LOOP_ALIGN();
+#endif
         const uint32_t* __restrict__ P = ptab + D.tab_off + 16u * r;
         uint32_t cv[8];
 #pragma unroll

@@ -92,19 +92,26 @@ def test_uniform_schedule_layouts(engine, oracle, mlen, d, c2, j, request):
 
 
 @pytest.mark.parametrize("mlen,d", [(61, 10), (61, 7), (62, 8), (62, 6), (125, 9), (126, 9)])
-def test_lane_table_layout(engine, oracle, mlen, d):
+def test_lane_table_layout(engine, oracle, mlen, d, request):
     """C2 = 3 (lane table): block B-1 holds 1-2 digits (message lengths =
     61, 62 mod 64), the lanes take block B's W_0/W_1 digits and keep its schedule in
-    registers, the loop walks the block B-1 values from the host's p-table.  AUTO picks it
-    for these lengths.  Per-nonce parity across loop-value (p-table entry) boundaries and
-    W_0 / W_1 roll-overs, and min parity over whole and partial rectangles."""
+    registers, the loop walks the block B-1 values from the p-table (k_ptab).  AUTO picks
+    it for these lengths once a search covers >= 2 block B-1 values; the parity windows
+    below are smaller, so they force it.  Per-nonce parity across loop-value (p-table
+    entry) boundaries and W_0 / W_1 roll-overs, and min parity over whole and partial
+    rectangles."""
+    import gpuhash
     rng = random.Random(mlen * 100 + d)
     m = bytes(rng.randrange(32, 127) for _ in range(mlen))
     nb1 = (mlen + 1) % 64 and 64 - (mlen + 1) % 64
     RQ = 10 ** (d - nb1)  # lane values per loop value
     lo_d, hi_d = 10 ** (d - 1), 10 ** d - 1
-    engine.min(m, lo_d, lo_d + 1000)
+    request.addfinalizer(lambda: engine.set_layout_policy(gpuhash.LAYOUT_AUTO))
+    engine.min(m, lo_d, lo_d + 3 * RQ)
     assert {(r["C2"], r["J"]) for r in engine.launches()} == {(3, 1)}, engine.launches()
+    engine.min(m, lo_d, lo_d + RQ // 2)
+    assert {(r["C2"], r["J"]) for r in engine.launches()} == {(1, 1)}, engine.launches()
+    engine.set_layout_policy(gpuhash.LAYOUT_LANETABLE)
     p = rng.randrange(lo_d // RQ + 1, hi_d // RQ)
     for lo in (p * RQ - 2500, p * RQ + RQ // 2 - 3333, p * RQ + 9_990_000 % RQ - 100):
         got = engine.hash_range(m, lo, 6000)

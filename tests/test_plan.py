@@ -113,10 +113,10 @@ def test_descriptor_replay_matches_oracle(hc, oracle, policy):
     hc.hostcheck_set_layout_policy(AUTO)
     # the reachable (J, C2, EX) variants of each policy were all exercised: 14 plain, 3
     # extra-block, the K+W table (C2 = 1, J = 0), and per policy the J = 1 straddles --
-    # UNIFORM: C2 = 2 and 3; AUTO: C2 = 3 (and 2 on searches of > 65536 block B-1 values,
-    # which this test's ranges rarely reach); CLASSIC: C2 = 1 only;
+    # UNIFORM: C2 = 2 and 3; AUTO: C2 = 1 (narrow searches) and 3 (and 2 on searches of
+    # > 65536 block B-1 values, which this test's ranges rarely reach); CLASSIC: C2 = 1;
     # LANETABLE: C2 = 3 only
-    want = {UNIFORM: {(1, 2, 0), (1, 3, 0)}, AUTO: {(1, 3, 0)},
+    want = {UNIFORM: {(1, 2, 0), (1, 3, 0)}, AUTO: {(1, 1, 0), (1, 3, 0)},
             CLASSIC: {(1, 1, 0)}, LANETABLE: {(1, 3, 0)}}[policy]
     straddle = {v for v in seen if v[0] == 1 and v[1] >= 1}
     assert straddle <= want | {(1, 2, 0)} and want - {(1, 2, 0)} <= straddle, sorted(seen)
@@ -126,7 +126,8 @@ def test_descriptor_replay_matches_oracle(hc, oracle, policy):
 def test_layout_policy_for_straddling_j1(hc):
     """J = 1 straddles (4 + q1 digits in block B's W_0/W_1, the rest in block B-1).  AUTO
     takes the lane table (C2 = 3) unless the search touches more than 65536 block B-1
-    values, then the two-word uniform loop (C2 = 2), whose rows are full there; CLASSIC
+    values, then the two-word uniform loop (C2 = 2), whose rows are full there, or spans
+    fewer than 2 block B-1 values, then the classic layout (C2 = 1); CLASSIC
     always C2 = 1, LANETABLE always C2 = 3, UNIFORM C2 = 2 whenever block B-1 holds >= 3
     digits (round 2's rule)."""
     pick = lambda m, a, b: {(l.J, l.C2) for l in plan(hc, m, a, b)}
@@ -139,6 +140,8 @@ def test_layout_policy_for_straddling_j1(hc):
     m56 = b"z" * 56
     assert pick(m56, lo, lo + 65000 * 10 ** 5) == {(1, 3)}
     assert pick(m56, lo, lo + 70000 * 10 ** 5) == {(1, 2)}
+    # fewer than 2 block B-1 values' worth of nonces: the classic layout
+    assert pick(m, lo, lo + 10 ** 8) == {(1, 1)} and pick(m, lo, lo + 2 * 10 ** 8) == {(1, 3)}
     try:
         hc.hostcheck_set_layout_policy(UNIFORM)
         assert pick(m, *narrow) == {(1, 2)}

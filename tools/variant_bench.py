@@ -26,7 +26,9 @@ with gpuhash.Engine([0], lib_path=sys.argv[1]) as e:
              ("j2", b"", 10**9, 10**9 + (1 << 31)),                # plain, early loop word
              ("cj1", b"c" * 61, 10**9, 10**9 + (1 << 31)),         # classic straddle C2=1, J=1
              ("u2f", b"u" * 58, 10240 * 10**7, 10240 * 10**7 + 256 * 10**7 - 1),  # C2=2, one full row
-             ("u2p", b"u" * 60, 10**9, (1 << 32) - 1)]  # C2=2, 430 lane values: wave 3 of row 2 idle
+             ("u2p", b"u" * 60, 10**9, (1 << 32) - 1),  # C2=2, 430 lane values: wave 3 of row 2 idle
+             ("lt61", b"t" * 61, 10**9, 10**9 + (1 << 31)),        # C2=3 lane table, 2 digits in B-1
+             ("lt58", b"t" * 58, 10**11, 10**11 + (1 << 32))]     # C2=3 lane table, 5 digits in B-1
     for name, msg, lo, hi in cases:
         e.min(msg, lo, hi)
         best, res = 1e9, None
