@@ -66,7 +66,7 @@ BIG = [
 # config 5 (BASELINE configs[4]): 16 clients "client-00".."client-15", each sending
 # Request(msg, 0, maxNonce = 2^36) -- inclusive, p1.pdf p.14; config 4 (configs[3]):
 # "bradfitz" over [0, 2^40).
-CFG5_CLIENTS = ["client-00", "client-05", "client-10", "client-15"]
+CFG5_CLIENTS = [f"client-{i:02d}" for i in range(16)]
 HUGE = [(f"cfg5_{c}_2p36", c.encode(), 0, 1 << 36, "config 5: one client's whole request")
         for c in CFG5_CLIENTS] + [
     ("cfg4_bradfitz_2p40", b"bradfitz", 0, (1 << 40) - 1, "config 4: [0, 2^40) of bradfitz"),

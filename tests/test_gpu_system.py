@@ -208,10 +208,10 @@ def test_config5_full_size(procs, engine, oracle, golden):
     """BASELINE configs[4] at full size on the one GPU (p1.pdf pp.14-15): 16 concurrent
     clients "client-00".."client-15", each Request(msg, 0, 2^36); 8 GPU-backed miners (4
     Python, 4 compiled) sharing the GPU; lspnet read and write drops of 10% on every role;
-    one miner SIGKILLed mid-job, whose job must be re-run.  Clients 00/05/10/15 are
-    checked against the CPU goldens of tests/golden/make_golden.py --huge (SHA-NI /
-    AVX-512 restatement over the whole [0, 2^36]); the others against one direct engine
-    search of the same range, plus an oracle re-hash of every printed winner."""
+    one miner SIGKILLed mid-job, whose job must be re-run.  Every client with a CPU golden
+    (tests/golden/make_golden.py --huge: the SHA-NI / AVX-512 restatement over the whole
+    [0, 2^36]) is checked against it; any other against one direct engine search of the
+    same range; every printed winner is re-hashed by the oracle."""
     import time as _t
     gold = {r["name"]: r for r in golden["ranges"]}
     port = free_port()
@@ -245,7 +245,7 @@ def test_config5_full_size(procs, engine, oracle, golden):
         else:
             assert (h, n) == engine.min(msg, 0, max_nonce), i
         assert oracle.hash(msg, n) == h
-    assert checked_golden == 4
+    assert checked_golden >= 4
     server.send_signal(signal.SIGTERM)
     log = server.communicate(timeout=30)[1]
     assert "lost; job [" in log and "requeued" in log, log[-2000:]
