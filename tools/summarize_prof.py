@@ -17,6 +17,7 @@ import json
 import os
 import re
 import shutil
+import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -29,16 +30,14 @@ def short(name: str) -> str:
 
 
 def load_pmc(d):
+    """{kernel: {counter: {dispatch: value}}} of one --pmc pass."""
     path = os.path.join(OUT, d, "pmc_counter_collection.csv")
     if not os.path.exists(path):
-        return {}, {}
-    vals = collections.defaultdict(lambda: collections.defaultdict(float))
-    disp = collections.defaultdict(set)
+        return {}
+    vals = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(float)))
     for r in csv.DictReader(open(path)):
-        k = short(r["Kernel_Name"])
-        vals[k][r["Counter_Name"]] += float(r["Counter_Value"])
-        disp[k].add(r["Dispatch_Id"])
-    return vals, {k: len(v) for k, v in disp.items()}
+        vals[short(r["Kernel_Name"])][r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    return vals
 
 
 def main():
@@ -55,16 +54,21 @@ def main():
     build_id = open(bid_path).read().strip() if os.path.exists(bid_path) else None
     summary = {"tag": tag, "build_id": build_id, "kernels": {}}
     traffic = {"source": f"profiles/{tag}_pmc_summary.json", "kernels": {}}
+    # per launch = the MEDIAN over the profiled dispatches of a kernel (round 3; rounds 1-2
+    # took the mean): one of three config-2 launches once read 79 MB of FETCH_SIZE against
+    # 2.3 MB for the other two (profiles/r03_pmc_summary.json keeps the max beside it)
     merged = collections.defaultdict(dict)
+    maxes = collections.defaultdict(dict)
     launches = {}
     for d in ("pmc1", "pmc2", "pmc3", "pmc4"):
-        v, n = load_pmc(d + sfx)
-        for k, cs in v.items():
-            for c, x in cs.items():
-                merged[k][c] = x / max(n[k], 1)
-            launches[k] = n[k]
+        for k, cs in load_pmc(d + sfx).items():
+            for c, per in cs.items():
+                xs = sorted(per.values())
+                merged[k][c] = statistics.median(xs)
+                maxes[k][c] = xs[-1]
+                launches[k] = len(xs)
     for k, cs in merged.items():
-        e = {"launches_profiled": launches.get(k), "per_launch": cs}
+        e = {"launches_profiled": launches.get(k), "per_launch": cs, "per_launch_max": maxes[k]}
         if "FETCH_SIZE" in cs or "WRITE_SIZE" in cs:
             hbm = (2.0 * cs.get("FETCH_SIZE", 0.0) + cs.get("WRITE_SIZE", 0.0)) * 1024.0
             e["hbm_bytes_per_launch"] = hbm
