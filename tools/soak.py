@@ -28,8 +28,11 @@ threads = min(16, len(os.sched_getaffinity(0)))
 
 def case():
     mlen = rng.choice([rng.randrange(0, 301)] * 9 + [rng.randrange(1000, 4097)])
-    m = bytes(rng.randrange(256) for _ in range(mlen))
     d = rng.randrange(1, 21)
+    if rng.random() < 0.25:  # round 3: the J = 1 straddles (lane table, two-word, classic)
+        mlen = 64 * rng.randrange(0, 4) + rng.choice([55, 56, 57, 58, 59, 60, 61, 62])
+        d = rng.randrange(6, 13)
+    m = bytes(rng.randrange(256) for _ in range(mlen))
     lo_d = 0 if d == 1 else 10 ** (d - 1)
     hi_d = U64 if d == 20 else 10 ** d - 1
     n = int(10 ** rng.uniform(0, 6.3))
@@ -46,7 +49,8 @@ count = nonces = 0
 with gpuhash.Engine([0]) as eng:
     while time.time() - t0 < seconds:
         m, lo, hi = case()
-        policy = rng.choice([gpuhash.LAYOUT_AUTO, gpuhash.LAYOUT_UNIFORM, gpuhash.LAYOUT_CLASSIC])
+        policy = rng.choice([gpuhash.LAYOUT_AUTO, gpuhash.LAYOUT_UNIFORM, gpuhash.LAYOUT_CLASSIC,
+                             gpuhash.LAYOUT_LANETABLE])
         eng.set_layout_policy(policy)
         got = eng.min(m, lo, hi)
         want = oracle.min(m, lo, hi, threads=threads)
