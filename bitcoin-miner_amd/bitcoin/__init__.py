@@ -72,10 +72,21 @@ def marshal(m: Message) -> bytes:
                            for k, v in d.items()) + "}").encode()
 
 
+_FOLD = str.maketrans("ABCDEFGHIJKLMNOPQRSTUVWXYZ", "abcdefghijklmnopqrstuvwxyz")
+
+
+def go_object(pairs) -> dict:
+    """json.loads object hook with encoding/json's field matching: a key selects the
+    struct field whose name equals it ignoring (ASCII) case, and the last such key in the
+    document wins; unknown keys of any shape are ignored by the callers.  Keys are stored
+    case-folded (csrc/lsp_native.h jfield does the same)."""
+    return {k.translate(_FOLD): v for k, v in pairs}
+
+
 def _u64(d: dict, key: str) -> int:
     """A uint64 field as Go's json.Unmarshal accepts it: an integer literal in
     [0, 2^64-1] (no fraction, exponent or sign); anything else fails the whole message."""
-    v = d.get(key, 0)
+    v = d.get(key.translate(_FOLD), 0)
     if v is None:
         return 0
     if isinstance(v, bool) or not isinstance(v, int) or not 0 <= v <= UINT64_MAX:
@@ -92,13 +103,13 @@ def unmarshal(raw: bytes) -> Message:
     if isinstance(raw, (bytes, bytearray)):
         # Go's decoder turns invalid UTF-8 into U+FFFD instead of failing the message
         raw = bytes(raw).decode("utf-8", "replace")
-    d = json.loads(raw)
+    d = json.loads(raw, object_pairs_hook=go_object)
     if not isinstance(d, dict):
         raise ValueError("json: cannot unmarshal non-object into Go value of type bitcoin.Message")
-    t = d.get("Type", 0)
+    t = d.get("type", 0)
     if isinstance(t, bool) or not isinstance(t, int):
         raise ValueError(f"json: cannot unmarshal {t!r} into Go struct field Message.Type")
-    data = d.get("Data", "")
+    data = d.get("data", "")
     if data is None:
         data = ""
     if not isinstance(data, str):

@@ -2,12 +2,9 @@
 // (miner_main.cpp, server_main.cpp).  Header-only; no HIP, no gpuhash types.
 //
 //   * JSON as Go's encoding/json reads and writes the two message types: lsp.Message
-//     (lsp/message.go:17-22) and bitcoin.Message (bitcoin/message.go:16-21).  Known
-//     divergences of the reader from json.Unmarshal, both on input the reference's own
-//     programs never write: an unknown key whose value is an object or array fails the
-//     whole message (Go skips unknown fields of any shape), and keys match
-//     case-sensitively (Go also accepts "type" for "Type").  Such a message is dropped, as
-//     Go drops a message it cannot decode;
+//     (lsp/message.go:17-22) and bitcoin.Message (bitcoin/message.go:16-21), including
+//     json.Unmarshal's leniencies: unknown fields of any shape are skipped, keys match
+//     field names ignoring (ASCII) case, and the last matching key wins;
 //   * lspnet's UDP endpoints with per-role drop injection (lspnet/conn.go:34-113,
 //     staff.go:14-58), the percentages taken from LSPNET_{CLIENT,SERVER}_{READ,WRITE}_DROP
 //     like the Python programs;
@@ -52,10 +49,33 @@ constexpr size_t kMaxDatagram = 2000;  // the reference reads into 2000-byte buf
 // JSON
 
 struct JVal {
-    enum Kind { Null, Bool, Num, Str } kind = Null;
+    enum Kind { Null, Bool, Num, Str, Composite } kind = Null;  // Composite: object or array
     std::string text;  // Str: the decoded UTF-8 bytes; Num: the literal
     bool b = false;
 };
+
+// The members of one JSON object in document order (duplicates kept).
+using JObj = std::vector<std::pair<std::string, JVal>>;
+
+// The value json.Unmarshal stores in struct field `name`: every key that equals the field
+// name ignoring ASCII case maps to it, and the last such key in the document wins (Go
+// decodes members in order; fields here never differ only by case).  nullptr if absent.
+inline const JVal* jfield(const JObj& o, const char* name) {
+    const JVal* v = nullptr;
+    const size_t n = std::strlen(name);
+    for (const auto& kv : o) {
+        if (kv.first.size() != n) continue;
+        bool eq = true;
+        for (size_t i = 0; i < n && eq; i++) {
+            char a = kv.first[i], b = name[i];
+            if (a >= 'A' && a <= 'Z') a = (char)(a - 'A' + 'a');
+            if (b >= 'A' && b <= 'Z') b = (char)(b - 'A' + 'a');
+            eq = a == b;
+        }
+        if (eq) v = &kv.second;
+    }
+    return v;
+}
 
 inline void put_utf8(std::string& out, uint32_t cp) {
     if (cp < 0x80) {
@@ -101,8 +121,9 @@ class JsonReader {
    public:
     explicit JsonReader(const std::string& s) : s_(s) {}
 
-    // A single JSON object whose values are scalars; false if malformed.
-    bool object(std::map<std::string, JVal>& out) {
+    // A single JSON object; members with object/array values (unknown fields, which Go
+    // skips) are kept as Composite.  false if malformed.
+    bool object(JObj& out) {
         ws();
         if (!eat('{')) return false;
         ws();
@@ -116,7 +137,7 @@ class JsonReader {
             ws();
             JVal v;
             if (!value(v)) return false;
-            out[key] = v;  // Go keeps the last duplicate too
+            out.emplace_back(std::move(key), std::move(v));
             ws();
             if (eat(',')) continue;
             if (eat('}')) return end();
@@ -224,18 +245,39 @@ class JsonReader {
             v.text = s_.substr(b, i_ - b);
             return true;
         }
-        return false;  // nested objects/arrays never appear in these messages
+        if (c == '{' || c == '[') { v.kind = JVal::Composite; return skip_composite(); }
+        return false;
+    }
+    // Skips one object or array (any nesting), validating its strings and brackets.
+    bool skip_composite() {
+        std::string close;
+        do {
+            ws();
+            if (i_ >= s_.size()) return false;
+            const char c = s_[i_];
+            if (c == '{' || c == '[') { close += c == '{' ? '}' : ']'; i_++; continue; }
+            if (c == '}' || c == ']') {
+                if (close.empty() || close.back() != c) return false;
+                close.pop_back();
+                i_++;
+                continue;
+            }
+            if (c == ',' || c == ':') { i_++; continue; }
+            JVal x;
+            if (!value(x)) return false;
+        } while (!close.empty());
+        return true;
     }
 };
 
 // A uint64 struct field as Go's json.Unmarshal fills it: a plain non-negative integer
 // literal <= 2^64-1; null (or absent) leaves the zero value.  Anything else fails.
-inline bool get_u64(const std::map<std::string, JVal>& o, const char* k, uint64_t& out) {
+inline bool get_u64(const JObj& o, const char* k, uint64_t& out) {
     out = 0;
-    auto it = o.find(k);
-    if (it == o.end() || it->second.kind == JVal::Null) return true;
-    if (it->second.kind != JVal::Num) return false;
-    const std::string& t = it->second.text;
+    const JVal* f = jfield(o, k);
+    if (!f || f->kind == JVal::Null) return true;
+    if (f->kind != JVal::Num) return false;
+    const std::string& t = f->text;
     if (t.empty() || t.size() > 20) return false;
     unsigned __int128 v = 0;
     for (char c : t) {
@@ -248,12 +290,12 @@ inline bool get_u64(const std::map<std::string, JVal>& o, const char* k, uint64_
     return true;
 }
 
-inline bool get_int(const std::map<std::string, JVal>& o, const char* k, long long& out) {
+inline bool get_int(const JObj& o, const char* k, long long& out) {
     out = 0;
-    auto it = o.find(k);
-    if (it == o.end() || it->second.kind == JVal::Null) return true;
-    if (it->second.kind != JVal::Num) return false;
-    const std::string& t = it->second.text;
+    const JVal* f = jfield(o, k);
+    if (!f || f->kind == JVal::Null) return true;
+    if (f->kind != JVal::Num) return false;
+    const std::string& t = f->text;
     size_t p = t[0] == '-' ? 1 : 0;
     if (p >= t.size() || t.size() - p > 18) return false;
     long long v = 0;
@@ -372,13 +414,13 @@ inline std::string lsp_marshal(const LspMsg& m) {
 }
 
 inline bool lsp_unmarshal(const std::string& raw, LspMsg& m) {
-    std::map<std::string, JVal> o;
+    JObj o;
     if (!JsonReader(raw).object(o)) return false;
     if (!get_int(o, "Type", m.type) || !get_int(o, "ConnID", m.conn) || !get_int(o, "SeqNum", m.seq)) return false;
-    auto it = o.find("Payload");
-    m.has_payload = it != o.end() && it->second.kind == JVal::Str;
-    if (it != o.end() && it->second.kind != JVal::Str && it->second.kind != JVal::Null) return false;
-    if (m.has_payload && !b64decode(it->second.text, m.payload)) return false;
+    const JVal* p = jfield(o, "Payload");
+    m.has_payload = p && p->kind == JVal::Str;
+    if (p && p->kind != JVal::Str && p->kind != JVal::Null) return false;
+    if (m.has_payload && !b64decode(p->text, m.payload)) return false;
     return true;
 }
 
@@ -394,13 +436,12 @@ struct BtcMsg {
 };
 
 inline bool btc_unmarshal(const std::string& raw, BtcMsg& m) {
-    std::map<std::string, JVal> o;
+    JObj o;
     if (!JsonReader(raw).object(o)) return false;
     if (!get_int(o, "Type", m.type)) return false;
-    auto it = o.find("Data");
-    if (it != o.end()) {
-        if (it->second.kind == JVal::Str) m.data = it->second.text;
-        else if (it->second.kind != JVal::Null) return false;
+    if (const JVal* d = jfield(o, "Data")) {
+        if (d->kind == JVal::Str) m.data = d->text;
+        else if (d->kind != JVal::Null) return false;
     }
     return get_u64(o, "Lower", m.lower) && get_u64(o, "Upper", m.upper) && get_u64(o, "Hash", m.hash) &&
            get_u64(o, "Nonce", m.nonce);

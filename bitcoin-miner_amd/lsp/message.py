@@ -33,9 +33,12 @@ class Message:
 
     @staticmethod
     def unmarshal(raw: bytes) -> "Message":
-        d = json.loads(raw)
-        p = d.get("Payload")
-        return Message(MsgType(int(d["Type"])), int(d.get("ConnID", 0)), int(d.get("SeqNum", 0)),
+        # encoding/json field matching: keys ignore (ASCII) case, the last one wins, unknown
+        # keys of any shape are skipped (as csrc/lsp_native.h)
+        d = json.loads(raw, object_pairs_hook=lambda pairs: {k.lower(): v for k, v in pairs
+                                                             if k.isascii()})
+        p = d.get("payload")
+        return Message(MsgType(int(d["type"])), int(d.get("connid", 0)), int(d.get("seqnum", 0)),
                        None if p is None else base64.b64decode(p))
 
     def __str__(self) -> str:  # message.go String()

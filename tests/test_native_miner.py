@@ -254,6 +254,11 @@ def test_empty_range_bad_json_and_unicode(san_miners, oracle):
     s.srv.Write(conn, bitcoin.marshal(bitcoin.NewRequest("msg", U64 - 500, U64)))
     r = s.result()
     assert (r.Hash, r.Nonce) == oracle.min(b"msg", U64 - 500, U64)
+    # encoding/json's leniencies: keys matched ignoring case (the last one wins), unknown
+    # fields of any shape skipped (p1.pdf p.12: min over n = 0..2 of "msg")
+    s.srv.Write(conn, b'{"type":1,"DATA":"msg","lower":0,"Upper":9,"upper":2,"x":{"a":[1,{"b":"}]"}]},"y":[]}')
+    r = s.result()
+    assert (r.Hash, r.Nonce) == (4754799531757243342, 1)
     s.srv.Close()
 
 

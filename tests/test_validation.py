@@ -373,3 +373,18 @@ def test_unmarshal_replaces_lone_surrogates_and_bad_utf8_like_go():
     assert bitcoin.unmarshal(b'{"Type":1,"Data":"x\xff\xfey","Lower":0,"Upper":5}').Data == "x��y"
     assert bserver.request_error(m.Data, 0, 5) is None
     assert m.Data.encode() == b"a\xef\xbf\xbdb\xef\xbf\xbdc"
+
+
+def test_unmarshal_field_matching_like_go():
+    """encoding/json matches keys to fields ignoring case (the last
+    matching key wins) and skips unknown fields of any shape; both the Python reader and
+    csrc/lsp_native.h now do (tests/test_native_miner.py drives the compiled one)."""
+    m = bitcoin.unmarshal(b'{"type":1,"DATA":"x","lower":3,"Upper":9,"extra":{"a":[1,{"b":"}"}]},"z":[]}')
+    assert (m.Type, m.Data, m.Lower, m.Upper) == (bitcoin.MsgType.Request, "x", 3, 9)
+    m = bitcoin.unmarshal(b'{"Type":1,"Upper":5,"upper":7}')
+    assert m.Upper == 7
+    with pytest.raises((ValueError, TypeError)):
+        bitcoin.unmarshal(b'{"Type":1,"Lower":{"x":1}}')  # a known field of the wrong shape
+    import lsp.message as lm
+    x = lm.Message.unmarshal(b'{"type":1,"connid":4,"SEQNUM":2,"payload":"eA==","n":{"q":[1]}}')
+    assert (x.Type, x.ConnID, x.SeqNum, x.Payload) == (lm.MsgType.MsgData, 4, 2, b"x")
