@@ -136,12 +136,17 @@ def cpu_baseline_multicore(seconds: float = 5.0) -> dict:
 PMC_SUMMARY = {"2": "r03_pmc_summary.json", "3": "r03c3_pmc_summary.json", "4": "r03c4_pmc_summary.json"}
 
 
-def pmc_source(config: str, key) -> tuple[dict | None, dict]:
+def pmc_source(config: str, key, launch_cycles: float | None = None) -> tuple[dict | None, dict]:
     """(per-kernel PMC entry or None, provenance).  PMC counters cannot be read inside
     this process, so they come from the committed rocprofv3 summary of the same bench
     command -- but only if that summary was collected on a library with this library's
     build id (the hash of its sources, gpuhash_version): after any source change the
-    values are stale and the fields they feed are null until the passes are re-run."""
+    values are stale and the fields they feed are null until the passes are re-run.
+    Its counters are per launch, so they also need a launch of the same size: with
+    `launch_cycles` (this run's dominant launch, HIP-event ms x in-kernel clock) the entry
+    is used only while the profiled launch's GPU cycles are within 0.8-1.25x of it (a
+    profiled run clocks a few per cent lower).  --inproc rehearsals and non-default
+    ranges launch other sizes of the same kernel."""
     import gpuhash
     lib_id = gpuhash.build_id()
     prov = {"file": None, "build_id": None, "library_build_id": lib_id, "used": False}
@@ -164,6 +169,13 @@ def pmc_source(config: str, key) -> tuple[dict | None, dict]:
     if e is None:
         prov["reason"] = "dominant kernel not in the summary"
         return None, prov
+    prof_cycles = e.get("gpu_cycles_per_launch")
+    if launch_cycles and prof_cycles:
+        ratio = launch_cycles / prof_cycles
+        if not 0.8 <= ratio <= 1.25:
+            prov["reason"] = (f"profiled launch is another size ({prof_cycles:.3g} GPU cycles vs "
+                              f"{launch_cycles:.3g} here): PMC-derived fields are null")
+            return None, prov
     prov["used"] = True
     return e, prov
 
@@ -229,7 +241,7 @@ def roofline(config: str, recs: list[dict]) -> dict:
     kernel_ghs = dom["nonces"] / (dom["ms"] * 1e-3) / 1e9
     sclk = dom["clk_ms"] / dom["ms"] if dom["ms"] > 0 else 0.0  # MHz, measured in the kernel
     peak_at_clk = 256 * 128 * sclk * 1e6 / 1e12  # the guide's peak at the measured clock
-    pmc, prov = pmc_source(config, key)
+    pmc, prov = pmc_source(config, key, avg_ms * 1e-3 * sclk * 1e6 if sclk > 0 else None)
     insts = pmc_issued(pmc)
     issued_per_nonce = insts * 64 / (dom["nonces"] / dom["n"]) if insts else None
     issued_T = kernel_ghs * issued_per_nonce / 1e3 if issued_per_nonce else None

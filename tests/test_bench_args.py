@@ -67,7 +67,7 @@ def test_per_device_picks_the_slowest_shard():
 
 
 def test_roofline_of_the_dominant_kernel(monkeypatch):
-    monkeypatch.setattr(bench, "pmc_source", lambda cfg, key: (None, {"used": False}))
+    monkeypatch.setattr(bench, "pmc_source", lambda cfg, key, cycles=None: (None, {"used": False}))
     recs = [_rec(0, 4, 1 << 32, 123.0), _rec(0, 2, 10**6, 5.0)]
     r = bench.roofline("2", recs)
     assert r["kernel"] == "k_scan<J=4,C2=0,EX=0,MODE=0>"

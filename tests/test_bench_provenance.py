@@ -24,10 +24,12 @@ def profile(tmp_path, monkeypatch):
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
     monkeypatch.setitem(bench.PMC_SUMMARY, "2", "x_pmc_summary.json")
 
-    def write(build_id):
-        (prof / "x_pmc_summary.json").write_text(json.dumps({
-            "tag": "x", "build_id": build_id,
-            "kernels": {KNAME: {"per_launch": {"SQ_INSTS_VALU": 1000.0}, "hbm_bytes_per_launch": 4096.0}}}))
+    def write(build_id, cycles=None):
+        e = {"per_launch": {"SQ_INSTS_VALU": 1000.0}, "hbm_bytes_per_launch": 4096.0}
+        if cycles is not None:
+            e["gpu_cycles_per_launch"] = cycles
+        (prof / "x_pmc_summary.json").write_text(json.dumps({"tag": "x", "build_id": build_id,
+                                                             "kernels": {KNAME: e}}))
     return write
 
 
@@ -48,6 +50,17 @@ def test_stale_or_unstamped_profile_gives_nulls(profile, stale):
     profile(stale)
     e, prov = bench.pmc_source("2", KEY)
     assert e is None and not prov["used"] and "different build" in prov["reason"]
+    assert bench.pmc_traffic(e) is None and bench.pmc_issued(e) is None
+
+
+def test_profile_of_another_launch_size_gives_nulls(profile):
+    # per-launch counters of a 2.9e8-cycle launch must not be divided by the nonces of a
+    # launch 6x longer (an --inproc rehearsal, a non-default range)
+    profile(gpuhash.build_id(), cycles=2.9e8)
+    e, prov = bench.pmc_source("2", KEY, launch_cycles=2.9e8 * 0.97)  # profiled clocks lower
+    assert prov["used"] and bench.pmc_issued(e) == 1000.0
+    e, prov = bench.pmc_source("2", KEY, launch_cycles=2.9e8 * 6.7)
+    assert e is None and not prov["used"] and "another size" in prov["reason"]
     assert bench.pmc_traffic(e) is None and bench.pmc_issued(e) is None
 
 
