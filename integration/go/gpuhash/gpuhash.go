@@ -33,8 +33,10 @@ type Error struct {
 func (e *Error) Error() string { return e.Msg }
 
 // IsArgument reports a deterministic argument error (GPUHASH_EINVAL, GPUHASH_ETOOLONG):
-// the same job fails the same way on every miner, so it must not be requeued.  Other
-// codes (ENODEV, EHIP, ENOMEM) are device or resource failures.
+// the same job fails the same way on every miner.  Other codes (ENODEV, EHIP, ENOMEM)
+// are device or resource failures.  The miner exits on either kind (miner.go): a server
+// pairs each Result with the miner's oldest job, so a skipped job would stay in flight;
+// the server's requeue cap then ends a job that fails on every miner.
 func (e *Error) IsArgument() bool {
 	return e.Code == int(C.GPUHASH_EINVAL) || e.Code == int(C.GPUHASH_ETOOLONG)
 }
