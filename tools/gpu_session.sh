@@ -2,7 +2,7 @@
 # tools/gpu_session.sh STEP... -- runs GPU steps on the gpurun box, each under its own
 # time limit, logging to gpurun_out/.  A plain failure (exit 1, e.g. a failing test)
 # lets the next step run; a fault, abort, segfault, time limit or kill stops the session.
-# Steps: family | inproc8c4 | valu | go | test | soak | smoke | bench | bench3 | bench4 | prof4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | pmc3 | pmc4 | sweep | variants | partial | regret | sys5
+# Steps: cumask | family | inproc8c4 | valu | go | test | soak | smoke | bench | bench3 | bench4 | prof4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | pmc3 | pmc4 | sweep | variants | partial | regret | sys5
 set -u
 cd "$(dirname "$0")/.."
 OUT=gpurun_out
@@ -51,6 +51,7 @@ for step in "$@"; do
         sys5c) run sys5c 900 python -u tools/system_bench.py --compiled ;;
         sys5a) run sys5a 900 python -u tools/system_bench.py --adaptive
                run sys5an 900 python -u tools/system_bench.py --adaptive --native ;;
+        cumask) run cumask 120 ./tools/bin/cumask_probe 20000 ;;
         family) run family 300 python3 -u tools/family_issue.py
                 cp "$OUT/family.log" "$OUT/fam.jsonl"
                 run family_pmc 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/fam_pmc" -o pmc --output-format csv -- python3 tools/family_issue.py --once
