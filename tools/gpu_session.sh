@@ -57,7 +57,7 @@ for step in "$@"; do
                 run family_pmc 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/fam_pmc" -o pmc --output-format csv -- python3 tools/family_issue.py --once
                 run family_sum 60 python3 tools/family_issue.py --summarize "$OUT/fam_pmc" "$OUT/fam.jsonl" ;;
         inproc8c4) run inproc8c4 300 python -u bench.py --inproc 0,0,0,0,0,0,0,0 --config 4 --steps 1 --warmup 1 --no-cpu-baseline ;;
-        soak) run soak 400 python -u tools/soak.py "${SOAK_SECONDS:-90}" "${SOAK_SEED:-2026}" ;;
+        soak) run soak $(( ${SOAK_SECONDS:-90} + 60 )) python -u tools/soak.py "${SOAK_SECONDS:-90}" "${SOAK_SEED:-2026}" ;;
         c4full) run c4full 400 python -u tools/config4_full.py ;;
         dist8c4) run dist8c4 400 env GPUHASH_SHARE_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29547 bench.py --gpus 8 --config 4 --steps 1 --warmup 0 ;;
         bench3) run bench3 300 python -u bench.py --config 3 --steps 5 --warmup 1 ;;
