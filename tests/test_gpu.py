@@ -218,6 +218,21 @@ def test_long_messages(engine, oracle, mlen):
         assert (engine.hash_range(m, lo, 3000) == oracle.hash_range(m, lo, 3000)).all()
 
 
+@pytest.mark.parametrize("short", [0, 5, 9, 19])
+def test_maximum_message_size(engine, oracle, short):
+    # The largest Data the ABI accepts (GPUHASH_MAX_MSG = 1 MiB = 16,384 whole blocks,
+    # compressed into the host midstate once per call), and 5 / 9 / 19 bytes less: m = 59,
+    # 55 and 45 mod 64 put the 10-digit nonces in the lane-table, K+W-table and
+    # extra-block layouts.  The naive C oracle re-hashes the whole MiB per nonce (hash.go
+    # has no midstate), so the ranges stay short.
+    import gpuhash
+    m = bytes((i * 2654435761 >> 13) & 0xFF for i in range(gpuhash.GPUHASH_MAX_MSG - short))
+    lo = 10 ** 9 - 32  # 9 -> 10 digits
+    assert (engine.hash_range(m, lo, 64) == oracle.hash_range(m, lo, 64)).all()
+    lo = 10 ** 12 - 256  # 12 -> 13 digits
+    assert engine.min(m, lo, lo + 511) == oracle.min(m, lo, lo + 511, threads=8)
+
+
 def test_single_nonce_ranges(engine, oracle):
     rng = random.Random(1)
     for n in [0, 1, 9, 10, 99, 100, 12345, 10 ** 9 - 1, 10 ** 9, 2 ** 32 - 1, 10 ** 19, U64 - 1, U64] + \

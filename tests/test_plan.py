@@ -166,10 +166,10 @@ def test_every_digit_count_and_message_length(hc, oracle, mlen):
                     assert desc_hash(hc, m, a, b, i, n) == oracle.hash(m, n)
 
 
-@pytest.mark.parametrize("mlen", [1000, 1299, 1300, 4093])
+@pytest.mark.parametrize("mlen", [1000, 1299, 1300, 4093, (1 << 20) - 5, 1 << 20])
 def test_long_messages(hc, oracle, mlen):
     # the LSP packet budget caps real messages near 1.3 KB; the host
-    # midstate covers every block before the digits
+    # midstate covers every block before the digits, up to GPUHASH_MAX_MSG = 1 MiB
     m = bytes((i * 131 + 7) % 256 for i in range(mlen))
     for d in (1, 9, 10, 12, 20):
         lo = 0 if d == 1 else 10 ** (d - 1)
