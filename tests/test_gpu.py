@@ -336,6 +336,17 @@ def test_multi_device_sharding_and_host_argmin(engine, oracle):
         assert multi.min(b"bradfitz", 0, 9999) == oracle.min(b"bradfitz", 0, 9999)
 
 
+def test_more_shards_than_nonces(oracle):
+    """8 device entries (the 8-GPU shape, on the box's one GPU) over ranges of 1-7 nonces:
+    the shards without nonces stay idle and the host argmin takes only the others."""
+    import gpuhash
+    with gpuhash.Engine([0] * 8) as multi:
+        for m, lo, hi in [(b"w", 7, 7), (b"z", 42, 43), (b"q", 0, 4), (b"r", 9, 15), (b"e", U64, U64),
+                          (b"msg", 0, 2)]:
+            assert multi.min(m, lo, hi) == oracle.min(m, lo, hi), (m, lo, hi)
+            assert 1 <= multi.stats()["ndevices"] <= min(8, hi - lo + 1)
+
+
 def test_multi_device_sliced(engine, oracle, monkeypatch):
     """Slices (gpuhash_min_ex) over several devices: each slice is sharded over the 3
     entries and merged into the running argmin."""
