@@ -19,8 +19,12 @@ SHA block), 2^32 nonces -- per GPU, i.e. gpuhash_min over the rank's shard plus 
 Inputs are resident on the device before timing (the message is a kernel argument;
 the nonce space is generated in registers), so value = whole-job nonces / max-over-
 ranks wall time of K steps.  Extra keys: roofline (dominant scan kernel, HIP-event
-timed in this run on the library's own stream) and cpu_baseline (oracle/ C restatement
-of the reference loop, timed on this host on a bounded sample, rank 0 at N=1 only).
+timed in this run on the library's own stream), cpu_baseline (oracle/ C restatement
+of the reference loop, timed on this host on a bounded sample, rank 0 at N=1 only), and
+search_2p40: after the timed steps, ONE search of 'bradfitz' over [0, 2^40) on the same
+N devices (north_star: "near-linear 1->8 GPU GH/s scaling on a 2^40-nonce search"), its
+time, GH/s, per-shard device ordinals, and its (hash, nonce) checked against the CPU
+golden (exit 3 on a mismatch).  ~33 s on one GPU, ~33/N s on N; --no-search skips it.
 """
 from __future__ import annotations
 
@@ -75,11 +79,43 @@ def _time_min(fn, seconds: float, n0: int) -> tuple[int, int, float]:
     return lo, n, time.perf_counter() - t
 
 
-def _threads() -> int:
+def _cgroup_cpus() -> float | None:
+    """CPUs' worth of time the cgroup v2 quota grants (cpu.max "quota period"), or None."""
     try:
-        return min(16, len(os.sched_getaffinity(0)))
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        return None if quota == "max" else int(quota) / int(period)
+    except (OSError, ValueError):
+        return None
+
+
+def host_cpus() -> dict:
+    """The host the CPU baselines ran on: nproc (every CPU of the machine), the CPUs this
+    process may run on (sched_getaffinity), the cgroup CPU quota if one is set, the CPU
+    model, and `usable` = the affinity count, lowered to the quota when a quota caps it
+    (threads beyond the quota would only time-slice)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        return min(16, os.cpu_count() or 1)
+        aff = os.cpu_count() or 1
+    quota = _cgroup_cpus()
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    return {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota, "model": model,
+            "usable": usable}
+
+
+def _threads() -> int:
+    """One worker per usable CPU (one goroutine per core)."""
+    return host_cpus()["usable"]
 
 
 def cpu_baseline(seconds: float = 12.0) -> dict:
@@ -115,7 +151,7 @@ def cpu_baseline_plain_c(seconds: float = 5.0) -> dict:
 
 def cpu_baseline_multicore(seconds: float = 5.0) -> dict:
     """The loop over contiguous per-thread sub-ranges (the SURVEY's 'one goroutine per
-    core' variant), threads = this process's CPU share capped at 16, OpenSSL SHA-256."""
+    core' variant), one thread per CPU in this process's affinity set, OpenSSL SHA-256."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import hash_oracle as ho
     threads = _threads()
@@ -127,6 +163,7 @@ def cpu_baseline_multicore(seconds: float = 5.0) -> dict:
         fn, what = (lambda a, z: c.min(MSG, a, z, threads=threads)), "oracle_min_mt (plain C)"
     lo, n, dt = _time_min(fn, seconds, 1 << 20)
     return {"value": n / dt / 1e9, "unit": "GH/s", "cores": threads, "kind": "port",
+            "host": host_cpus(),
             "sample": f"{what} over bradfitz [{lo}, {PER_GPU - 1}] ({n} nonces), {dt:.1f} s"}
 
 
@@ -314,6 +351,117 @@ def base_line(args, value: float, n: int, dt: float, workload: str, msg: bytes, 
     }
 
 
+# ---- the north_star's 2^40 search (BASELINE configs[3]) at every N ----
+#
+# After the timed steps, one search of `bradfitz` over [0, 2^40) -- the range the
+# north_star's "near-linear 1->8 GPU GH/s scaling on a 2^40-nonce search" names -- on the
+# same devices: in-process, one gpuhash_min over the context's devices (cost-balanced
+# shards, a host thread + stream each, host argmin); under torchrun, each rank's
+# cost-balanced window (gpuhash.dist.split_range) and the 24-byte gloo merge.  The result
+# is checked against the CPU golden of the same range (tests/golden/golden.json,
+# cfg4_bradfitz_2p40, computed by oracle/golden_scan.c), so the line proves the search
+# bit-exact at every N; a mismatch exits non-zero after the line is printed.
+SEARCH_DEFAULT = (0, (1 << 40) - 1)
+GOLDEN_PATH = os.path.join(ROOT, "tests", "golden", "golden.json")
+
+
+def parse_search(s: str):
+    """--search: "LO:HI" (inclusive, ints; "2^40" style powers allowed) or "off"."""
+    if s == "off":
+        return None
+
+    def num(x: str) -> int:
+        x = x.strip()
+        if "^" in x:  # "2^40-1"
+            base, rest = x.split("^", 1)
+            sub = 0
+            if "-" in rest:
+                rest, sub = rest.split("-", 1)
+                sub = int(sub)
+            return int(base) ** int(rest) - sub
+        return int(x)
+    lo, hi = (num(x) for x in s.split(":"))
+    if not 0 <= lo <= hi < 1 << 64:
+        raise ValueError(f"--search {s}: need 0 <= LO <= HI < 2^64")
+    return lo, hi
+
+
+def golden_for(msg: bytes, lo: int, hi: int):
+    """((hash, nonce), name) of the committed CPU golden for exactly this range, or
+    (None, None).  The fixture travels with the repo; nothing here reads the reference."""
+    try:
+        with open(GOLDEN_PATH) as f:
+            g = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    for r in g.get("ranges", []):
+        if r.get("msg_hex") == msg.hex() and r.get("lower") == lo and r.get("upper") == hi:
+            return (int(r["hash"]), int(r["nonce"])), r["name"]
+    return None, None
+
+
+def shard_rows(recs: list[dict]) -> list[dict]:
+    """Per shard (position in the context's device list) of one gpuhash_min call: its HIP
+    ordinal, the ordinal the runtime reports for its stream, the nonce windows it searched
+    (one per slice), its scan-kernel time and rate.  Every record of one slice of a shard
+    carries that slice's [lo, hi]."""
+    by = {}
+    for r in recs:
+        e = by.setdefault(r["shard"], {"shard": r["shard"], "device": r["device"],
+                                       "stream_devices": set(), "windows": set(), "kernel_ms": 0.0})
+        e["stream_devices"].add(r["stream_device"])
+        e["windows"].add((r["lo"], r["hi"]))
+        e["kernel_ms"] += r["ms"]
+    rows = []
+    for k in sorted(by):
+        e = by[k]
+        wins = sorted(e["windows"])
+        nonces = sum(b - a + 1 for a, b in wins)
+        rows.append({"shard": k, "device": e["device"], "stream_device": sorted(e["stream_devices"]),
+                     "lo": wins[0][0], "hi": wins[-1][1], "slices": len(wins), "nonces": nonces,
+                     "kernel_ms": round(e["kernel_ms"], 3),
+                     "kernel_GHs": round(nonces / (e["kernel_ms"] * 1e-3) / 1e9, 4) if e["kernel_ms"] else None})
+    return rows
+
+
+def check_shards(rows: list[dict], devs: list[int]) -> list[str]:
+    """Device evidence of a search's shards: shard k ran on devs[k] (the record's ordinal and
+    the stream's runtime ordinal agree with it), the shards' windows tile the search in
+    order, and -- when the device list has no repeats -- every shard ran on a different
+    device.  Returns the problems found (empty = fine)."""
+    bad = []
+    for r in rows:
+        if r["shard"] >= len(devs) or r["device"] != devs[r["shard"]]:
+            bad.append(f"shard {r['shard']} reports device {r['device']}, context lists {devs}")
+        if r["stream_device"] != [r["device"]]:
+            bad.append(f"shard {r['shard']} stream on device(s) {r['stream_device']}, not {r['device']}")
+    if len(set(devs)) == len(devs) and len({r["device"] for r in rows}) != len(rows):
+        bad.append("distinct devices requested but shards share a device")
+    return bad
+
+
+def search_line(res, dt: float, n: int, lo: int, hi: int, mode: str, devices, shards) -> dict:
+    want, name = golden_for(MSG, lo, hi)
+    total = hi - lo + 1
+    return {"msg": MSG.decode(), "range": [lo, hi], "nonces": total, "mode": mode,
+            "seconds": round(dt, 3), "GHs": round(total / dt / 1e9, 4),
+            "per_gpu_GHs": round(total / dt / 1e9 / n, 4), "n_gpus": n, "devices": devices,
+            "result": list(res), "golden": list(want) if want else None, "golden_name": name,
+            "matches_golden": (tuple(res) == want) if want else None, "shards": shards}
+
+
+def search_exit(out: dict, problems: list[str]) -> None:
+    """Non-zero exit AFTER the line is printed when the search missed its golden or a shard
+    ran somewhere other than its device: the line stays readable, the run counts as failed."""
+    s = out.get("search_2p40")
+    if s is not None and s["matches_golden"] is False:
+        print(f"bench.py: search {s['range']} returned {s['result']}, golden {s['golden']}", file=sys.stderr)
+        sys.exit(3)
+    if problems:
+        print("bench.py: device check failed: " + "; ".join(problems), file=sys.stderr)
+        sys.exit(3)
+
+
 def add_cpu_baselines(out: dict, args) -> None:
     if not args.no_cpu_baseline and args.config == "2":
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
@@ -382,10 +530,25 @@ def main_inproc(args, devs: list[int]) -> None:
     out["launches_per_step"] = len(recs) // max(args.steps, 1)
     out["roofline"] = roofline(args.config, slow_recs)
     out["roofline"]["device"] = slow
+    out["shards"] = shard_rows(recs)  # device evidence of the timed steps (kernel_ms over all K)
+    problems = check_shards(out["shards"], devs)
+    if args.search is not None:
+        lo, hi = args.search
+        barrier()
+        t0 = time.perf_counter()
+        sres = eng.min(MSG, lo, hi)
+        barrier()
+        sdt = time.perf_counter() - t0
+        rows = shard_rows(eng.launches())
+        problems += check_shards(rows, devs)
+        out["search_2p40"] = search_line(sres, sdt, n, lo, hi, "inproc", devs, rows)
+    if problems:
+        out["device_check"] = problems
     if n == 1:
         add_cpu_baselines(out, args)
     emit(out)
     eng.close()
+    search_exit(out, problems)
 
 
 def main_ranks(args, world: int, rank: int, local: int) -> None:
@@ -445,17 +608,54 @@ def main_ranks(args, world: int, rank: int, local: int) -> None:
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     roof = roofline(args.config, recs)
+    # device evidence of every rank: its shard of the timed steps ran on LOCAL_RANK's device
+    mine = shard_rows(recs)
+    problems = check_shards(mine, [local])
+    search = None
+    if args.search is not None:
+        from gpuhash.dist import split_range
+        lo, hi = args.search
+        win = split_range(lo, hi, world, msg_len=len(MSG))[rank]  # the engine's cost model
+        barrier()
+        t0 = time.perf_counter()
+        sres = eng.min(MSG, *win) if win is not None else None
+        sres = merge_min(gather_results(sres, coll_dev))
+        barrier()
+        sdt = time.perf_counter() - t0
+        t = torch.tensor([sdt], dtype=torch.float64, device=coll_dev or "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        sdt = float(t.item())
+        srows = shard_rows(eng.launches()) if win is not None else []
+        problems += check_shards(srows, [local])
+        for r in srows:  # one process per GPU: the rank is the shard
+            r["shard"] = rank
+        search = (sres, sdt, srows)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, {"rank": rank, "local_rank": local, "problems": problems,
+                                      "search_shards": search[2] if search else None})
     if rank == 0:
         value = per_gpu * world * args.steps / dt / 1e9
         out = base_line(args, value, world, dt, cfg["desc"], msg, f"dp{world}", "weak",
                         nonces_per_gpu=per_gpu, processes=world, backend=backend)
         out["result"] = list(res)  # (hash, nonce) argmin over every rank's windows
         out["roofline"] = roof
+        problems = [f"rank {g['rank']}: {p}" for g in gathered for p in g["problems"]]
+        if search is not None:
+            shards = [s for g in gathered for s in (g["search_shards"] or [])]
+            devices = [g["local_rank"] for g in gathered]
+            out["search_2p40"] = search_line(search[0], search[1], world, *args.search,
+                                             f"ranks ({backend} merge)", devices, shards)
+            if not shared and len({s["device"] for s in shards}) != len(shards):
+                problems.append("ranks on distinct GPUs but search shards share a device")
+        if problems:
+            out["device_check"] = problems
         if world == 1:
             add_cpu_baselines(out, args)
         emit(out)
     eng.close()
     dist.destroy_process_group()
+    if rank == 0:
+        search_exit(out, problems)
 
 
 def main() -> None:
@@ -472,9 +672,18 @@ def main() -> None:
     ap.add_argument("--inproc", default=None, metavar="DEVICES",
                     help="explicit device list for the one-process path (comma list, ordinals "
                          "may repeat to rehearse N shards on one GPU); overrides --gpus")
+    ap.add_argument("--search", default="0:2^40-1", metavar="LO:HI|off",
+                    help="after the timed steps, one search of 'bradfitz' over [LO, HI] on the "
+                         "same devices, checked against the committed CPU golden of that range "
+                         "(default: the north_star's 2^40-nonce search; 'off' skips it)")
+    ap.add_argument("--no-search", action="store_true", help="same as --search off")
     args = ap.parse_args()
     if args.gpus < 1:
         fail("--gpus must be >= 1")
+    try:
+        args.search = None if args.no_search else parse_search(args.search)
+    except ValueError as e:
+        fail(str(e))
     _quiet_stdout()
     # torch before libgpuhash: both link libamdhip64, and the process must load torch's
     # HIP runtime first, or torch later finds "No HIP GPUs are available"

@@ -104,18 +104,19 @@ def request_error(data: str, lower: int, upper: int) -> str | None:
     if n > GPUHASH_MAX_MSG:
         return f"Data is {n} bytes, over the engine's {GPUHASH_MAX_MSG}"
     # every job Request this server cuts from it must fit one LSP datagram (the reference
-    # reads 2000-byte buffers, lspnet/conn.go:35): a job's bounds can have 20 digits where
-    # the client sent Lower = 0, so a request that fit may yield jobs that do not, and a
+    # reads 2000-byte buffers, lspnet/conn.go:35): a job's bounds can have more digits than
+    # the client's Lower, so a request that fit may yield jobs that do not, and a
     # truncated datagram is never acked -- the job would hang
-    if len(job_frame_worst_case(data)) > lspnet.MAX_DATAGRAM:
+    if len(job_frame_worst_case(data, upper)) > lspnet.MAX_DATAGRAM:
         return f"its jobs would not fit a {lspnet.MAX_DATAGRAM}-byte LSP datagram"
     return None
 
 
-def job_frame_worst_case(data: str) -> bytes:
-    """The longest LSP frame a job of this request can take: both bounds at 20 digits,
-    10-digit ConnID and SeqNum."""
-    return lsp.message.NewData(2**31 - 1, 2**31 - 1, marshal(NewRequest(data, UINT64_MAX, UINT64_MAX))).marshal()
+def job_frame_worst_case(data: str, upper: int = UINT64_MAX) -> bytes:
+    """The longest LSP frame a job of this request can take: no job bound exceeds the
+    request's Upper, so both bounds at Upper's digit count (pricing them at
+    2^64-1 refused requests the reference serves), 10-digit ConnID and SeqNum."""
+    return lsp.message.NewData(2**31 - 1, 2**31 - 1, marshal(NewRequest(data, upper, upper))).marshal()
 
 
 @dataclass

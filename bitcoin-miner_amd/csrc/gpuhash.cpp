@@ -33,6 +33,8 @@ constexpr size_t kCounterBytes = 40;
 
 struct Dev {
     int ord = -1;
+    int shard = -1;        // position in gpuhash_open's device list
+    int stream_dev = -1;   // ordinal the runtime reports for `stream` (hipStreamGetDevice)
     hipStream_t stream = nullptr;
     unsigned long long* d_thresh = nullptr;
     Cand* d_cands = nullptr;
@@ -94,11 +96,16 @@ struct DeviceGuard {
         if ((expr) != hipSuccess) return GPUHASH_EHIP; \
     } while (0)
 
-static int dev_init(Dev& d, int ord) {
+static int dev_init(Dev& d, int ord, int shard) {
     d.ord = ord;
+    d.shard = shard;
     DeviceGuard guard;
     HIPCHK(hipSetDevice(ord));
     HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    hipDevice_t sd = -1;
+    HIPCHK(hipStreamGetDevice(d.stream, &sd));
+    if (sd != ord) return GPUHASH_EHIP;  // the stream must live on the device it serves
+    d.stream_dev = sd;
     if (hipMalloc(&d.d_thresh, sizeof(unsigned long long)) != hipSuccess) return GPUHASH_ENOMEM;
     if (hipMalloc(&d.d_ncand, sizeof(unsigned int)) != hipSuccess) return GPUHASH_ENOMEM;
     if (hipMalloc(&d.d_best, sizeof(Cand)) != hipSuccess) return GPUHASH_ENOMEM;
@@ -337,7 +344,8 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
         const double ticks = (double)(c[2] - c[0]), rt = (double)(c[3] - c[1]);
         const double sclk = rt > 0 ? ticks / rt * 100.0 : 0.0;  // s_memrealtime runs at 100 MHz
         d.recs.push_back(gpuhash_launch_record{d.ord, groups[g].J, groups[g].C2, groups[g].EX,
-                                               big->d, big->c, nonces, (double)ms, sclk});
+                                               big->d, big->c, d.shard, d.stream_dev, lo, hi,
+                                               nonces, (double)ms, sclk});
     }
     d.launches = (uint32_t)groups.size();
     d.best_h = d.h_best->hash;
@@ -389,7 +397,7 @@ static int open_impl(const int* devices, int ndevices, gpuhash_ctx** out) {
     });
     ctx->devs.resize(ords.size());
     for (size_t i = 0; i < ords.size(); i++) {
-        int rc = dev_init(ctx->devs[i], ords[i]);
+        int rc = dev_init(ctx->devs[i], ords[i], (int)i);
         if (rc) return rc;
     }
     *out = ctx.release();

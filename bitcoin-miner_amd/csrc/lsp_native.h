@@ -57,11 +57,13 @@ struct JVal {
 // The members of one JSON object in document order (duplicates kept).
 using JObj = std::vector<std::pair<std::string, JVal>>;
 
-// The value json.Unmarshal stores in struct field `name`: every key that equals the field
-// name ignoring ASCII case maps to it, and the last such key in the document wins (Go
-// decodes members in order; fields here never differ only by case).  nullptr if absent.
-inline const JVal* jfield(const JObj& o, const char* name) {
-    const JVal* v = nullptr;
+// Calls f(value) for every member whose key equals struct field `name` ignoring ASCII
+// case, in document order, stopping at the first f that returns false.  Go's
+// json.Unmarshal decodes EVERY such member into the field in order: a null member leaves
+// the field as an earlier one set it, and a member of the wrong type fails the message
+// even if a later member is fine (it keeps the first UnmarshalTypeError).
+template <class F>
+inline bool jfields(const JObj& o, const char* name, F&& f) {
     const size_t n = std::strlen(name);
     for (const auto& kv : o) {
         if (kv.first.size() != n) continue;
@@ -72,9 +74,9 @@ inline const JVal* jfield(const JObj& o, const char* name) {
             if (b >= 'A' && b <= 'Z') b = (char)(b - 'A' + 'a');
             eq = a == b;
         }
-        if (eq) v = &kv.second;
+        if (eq && !f(kv.second)) return false;
     }
-    return v;
+    return true;
 }
 
 inline void put_utf8(std::string& out, uint32_t cp) {
@@ -237,74 +239,118 @@ class JsonReader {
         if (lit("null")) { v.kind = JVal::Null; return true; }
         if (lit("true")) { v.kind = JVal::Bool; v.b = true; return true; }
         if (lit("false")) { v.kind = JVal::Bool; v.b = false; return true; }
-        if (c == '-' || (c >= '0' && c <= '9')) {
+        if (c == '-' || (c >= '0' && c <= '9')) {  // RFC 8259 number, as Go's scanner
             size_t b = i_;
-            if (c == '-') i_++;
-            while (i_ < s_.size() && std::strchr("0123456789.eE+-", s_[i_])) i_++;
+            eat('-');
+            if (eat('0')) {
+            } else if (!digits()) {
+                return false;
+            }
+            if (eat('.') && !digits()) return false;
+            if (eat('e') || eat('E')) {
+                if (!eat('+')) eat('-');
+                if (!digits()) return false;
+            }
             v.kind = JVal::Num;
             v.text = s_.substr(b, i_ - b);
             return true;
         }
-        if (c == '{' || c == '[') { v.kind = JVal::Composite; return skip_composite(); }
+        if (c == '{' || c == '[') { v.kind = JVal::Composite; return composite(); }
         return false;
     }
-    // Skips one object or array (any nesting), validating its strings and brackets.
-    bool skip_composite() {
-        std::string close;
-        do {
+    bool digits() {  // [0-9]+
+        const size_t b = i_;
+        while (i_ < s_.size() && s_[i_] >= '0' && s_[i_] <= '9') i_++;
+        return i_ > b;
+    }
+    // Skips one object or array (any nesting) with the full grammar -- keys, colons and
+    // separators checked -- so a document Go's Unmarshal rejects ([1 2], {1:2}, {"a"},
+    // [,,]) is rejected here too.  Depth is bounded by the 2000-byte datagram.
+    bool composite() {
+        if (eat('[')) {
             ws();
-            if (i_ >= s_.size()) return false;
-            const char c = s_[i_];
-            if (c == '{' || c == '[') { close += c == '{' ? '}' : ']'; i_++; continue; }
-            if (c == '}' || c == ']') {
-                if (close.empty() || close.back() != c) return false;
-                close.pop_back();
-                i_++;
-                continue;
+            if (eat(']')) return true;
+            for (;;) {
+                ws();
+                JVal x;
+                if (!value(x)) return false;
+                ws();
+                if (eat(',')) continue;
+                return eat(']');
             }
-            if (c == ',' || c == ':') { i_++; continue; }
+        }
+        if (!eat('{')) return false;
+        ws();
+        if (eat('}')) return true;
+        for (;;) {
+            ws();
+            std::string key;
+            if (!string(key)) return false;
+            ws();
+            if (!eat(':')) return false;
+            ws();
             JVal x;
             if (!value(x)) return false;
-        } while (!close.empty());
-        return true;
+            ws();
+            if (eat(',')) continue;
+            return eat('}');
+        }
     }
 };
 
-// A uint64 struct field as Go's json.Unmarshal fills it: a plain non-negative integer
-// literal <= 2^64-1; null (or absent) leaves the zero value.  Anything else fails.
+// A uint64 struct field as Go's json.Unmarshal fills it: every matching member a plain
+// non-negative integer literal <= 2^64-1 (strconv.ParseUint) or null; the last non-null
+// one wins, absent or all-null leaves the zero value.  Anything else fails the message.
 inline bool get_u64(const JObj& o, const char* k, uint64_t& out) {
     out = 0;
-    const JVal* f = jfield(o, k);
-    if (!f || f->kind == JVal::Null) return true;
-    if (f->kind != JVal::Num) return false;
-    const std::string& t = f->text;
-    if (t.empty() || t.size() > 20) return false;
-    unsigned __int128 v = 0;
-    for (char c : t) {
-        if (c < '0' || c > '9') return false;
-        v = v * 10 + (unsigned)(c - '0');
-    }
-    if (t.size() > 1 && t[0] == '0') return false;  // not a JSON number
-    if (v > (unsigned __int128)kU64Max) return false;
-    out = (uint64_t)v;
-    return true;
+    return jfields(o, k, [&](const JVal& f) {
+        if (f.kind == JVal::Null) return true;
+        if (f.kind != JVal::Num) return false;
+        const std::string& t = f.text;
+        if (t.empty() || t.size() > 20) return false;
+        unsigned __int128 v = 0;
+        for (char c : t) {
+            if (c < '0' || c > '9') return false;
+            v = v * 10 + (unsigned)(c - '0');
+        }
+        if (v > (unsigned __int128)kU64Max) return false;
+        out = (uint64_t)v;
+        return true;
+    });
 }
 
+// An int (64-bit) struct field: strconv.ParseInt(literal, 10, 64), same member rules.
 inline bool get_int(const JObj& o, const char* k, long long& out) {
     out = 0;
-    const JVal* f = jfield(o, k);
-    if (!f || f->kind == JVal::Null) return true;
-    if (f->kind != JVal::Num) return false;
-    const std::string& t = f->text;
-    size_t p = t[0] == '-' ? 1 : 0;
-    if (p >= t.size() || t.size() - p > 18) return false;
-    long long v = 0;
-    for (size_t i = p; i < t.size(); i++) {
-        if (t[i] < '0' || t[i] > '9') return false;
-        v = v * 10 + (t[i] - '0');
-    }
-    out = p ? -v : v;
-    return true;
+    return jfields(o, k, [&](const JVal& f) {
+        if (f.kind == JVal::Null) return true;
+        if (f.kind != JVal::Num) return false;
+        const std::string& t = f.text;
+        const size_t p = t[0] == '-' ? 1 : 0;
+        if (p >= t.size() || t.size() - p > 19) return false;
+        __int128 v = 0;
+        for (size_t i = p; i < t.size(); i++) {
+            if (t[i] < '0' || t[i] > '9') return false;
+            v = v * 10 + (t[i] - '0');
+        }
+        if (p) v = -v;
+        if (v > (__int128)INT64_MAX || v < (__int128)INT64_MIN) return false;
+        out = (long long)v;
+        return true;
+    });
+}
+
+// A string ([]byte for LSP payloads) field: every matching member a string or null, the
+// last string wins; `set` false if none was.
+inline bool get_str(const JObj& o, const char* k, std::string& out, bool& set) {
+    set = false;
+    return jfields(o, k, [&](const JVal& f) {
+        if (f.kind == JVal::Null) return true;
+        if (f.kind != JVal::Str) return false;
+        out = f.text;
+        set = true;
+        return true;
+    });
 }
 
 // A string as Go's encoding/json writes it (encodeState.string): \" \\ \n \r \t, other
@@ -417,11 +463,15 @@ inline bool lsp_unmarshal(const std::string& raw, LspMsg& m) {
     JObj o;
     if (!JsonReader(raw).object(o)) return false;
     if (!get_int(o, "Type", m.type) || !get_int(o, "ConnID", m.conn) || !get_int(o, "SeqNum", m.seq)) return false;
-    const JVal* p = jfield(o, "Payload");
-    m.has_payload = p && p->kind == JVal::Str;
-    if (p && p->kind != JVal::Str && p->kind != JVal::Null) return false;
-    if (m.has_payload && !b64decode(p->text, m.payload)) return false;
-    return true;
+    // []byte: each string member is base64-decoded in order (an invalid one fails the
+    // message), null leaves the previous value
+    m.has_payload = false;
+    return jfields(o, "Payload", [&](const JVal& f) {
+        if (f.kind == JVal::Null) return true;
+        if (f.kind != JVal::Str || !b64decode(f.text, m.payload)) return false;
+        m.has_payload = true;
+        return true;
+    });
 }
 
 // ---------------------------------------------------------------------------------
@@ -439,10 +489,8 @@ inline bool btc_unmarshal(const std::string& raw, BtcMsg& m) {
     JObj o;
     if (!JsonReader(raw).object(o)) return false;
     if (!get_int(o, "Type", m.type)) return false;
-    if (const JVal* d = jfield(o, "Data")) {
-        if (d->kind == JVal::Str) m.data = d->text;
-        else if (d->kind != JVal::Null) return false;
-    }
+    bool set;
+    if (!get_str(o, "Data", m.data, set)) return false;
     return get_u64(o, "Lower", m.lower) && get_u64(o, "Upper", m.upper) && get_u64(o, "Hash", m.hash) &&
            get_u64(o, "Nonce", m.nonce);
 }

@@ -147,24 +147,26 @@ GroupLayout layout_for(uint64_t m, int d, uint64_t span = 0, int policy = kLayou
     //                       over the block B-1 values whose chaining values the host
     //                       precomputes: 44-46.3 GH/s, >= C2 = 2 on every measured layout,
     //                       full rows included (profiles/r03_sweep_lt_vs_u2.jsonl).
-    // AUTO takes C2 = 3 unless the search touches more than kMaxLtTable block B-1 values
-    // (its table: 64 B and one compression per value), where C2 = 2 rows are full anyway,
-    // or fewer than ~2 (a row's schedule build would not amortise): C2 = 1 there.  UNIFORM keeps the round-2 rule (C2 = 2 whenever block B-1 holds >= 3
-    // digits), CLASSIC and LANETABLE force their layout (tuning and parity tests).
+    // The policy rule is stated once, in include/gpuhash.h above GPUHASH_LAYOUT_AUTO
+    // (tests/test_plan.py checks this function against it): the lane table's p-table
+    // costs 64 B and one compression per block B-1 value, so AUTO and LANETABLE cap it at
+    // kMaxLtTable (= GPUHASH_LANETABLE_MAX) values, beyond which C2 = 2 rows are full anyway.
     if (g.C2 && g.J == 1) {
         const int nb1 = d - 4 - g.q;  // digits in block B-1 and earlier
         const uint64_t RQ = pow10u(4 + g.q);
         const uint64_t nloop = span ? (span - 1) / RQ + 2 : pow10u(std::min(nb1, 6));
+        const bool lt_too_big = nb1 >= 3 && nloop > kMaxLtTable;
         int c2 = 3;
         if (policy == kLayoutClassic) c2 = 1;
         else if (policy == kLayoutUniform) c2 = nb1 >= 3 ? 2 : 3;
-        else if (policy == kLayoutAuto) {
+        else if (policy == kLayoutLaneTable) c2 = lt_too_big ? 2 : 3;
+        else {
             // a row of the lane table builds block B's schedule once (~550 VALU) for every
             // loop value it then hashes: below ~2 loop values the classic layout's
             // per-nonce schedule (~1,300 VALU per nonce) is cheaper
             // (profiles/r03_planner_regret.jsonl: 26.2 vs 29.0 GH/s at 0.7 loop values)
             if (span && span < 2 * RQ) c2 = 1;
-            else c2 = (nb1 >= 3 && nloop > kMaxLtTable) ? 2 : 3;
+            else c2 = lt_too_big ? 2 : 3;
         }
         if (c2 == 2) {
             g.C2 = 2;

@@ -36,6 +36,8 @@
 
 #include <vector>
 
+#include "gpuhash.h"  // GPUHASH_LANETABLE_MAX: the layout-policy rule is stated there
+
 namespace gpuhash {
 
 static constexpr uint32_t kIV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
@@ -97,17 +99,13 @@ static constexpr int kMaxLaunchDigits = 10;   // s + q <= 10  -> <= 10^10 nonces
 // C2 = 2 launches: s + q <= 12 still keeps rows * R = ceil(10^s / 256) * 10^q < 2^32
 static constexpr int kMaxLaunchDigitsU2 = 12;
 
-// Choice between the J = 1 straddling layouts (plan.cpp layout_for):
-//   auto       C2 = 3 (lane table), or C2 = 2 (uniform two-word loop) when the search
-//              touches more than kMaxLtTable block B-1 values
-//   uniform    C2 = 2 whenever block B-1 holds >= 3 digits, else C2 = 3 (tuning / tests)
-//   classic    C2 = 1: lanes in W_0 and block B-1, per-nonce schedule (tuning / tests)
-//   lanetable  C2 = 3 always (tuning / tests)
+// Choice between the J = 1 straddling layouts (plan.cpp layout_for); the rule is stated
+// once, in include/gpuhash.h above GPUHASH_LAYOUT_AUTO.
 enum LayoutPolicy { kLayoutAuto = 0, kLayoutUniform = 1, kLayoutClassic = 2, kLayoutLaneTable = 3 };
-// C2 = 3: at most this many loop values (p-table entries) per launch, and AUTO takes the
-// layout only for searches touching at most kMaxLtTable block B-1 values (4 MB of table)
+// C2 = 3: at most this many loop values (p-table entries) per launch, and AUTO / LANETABLE
+// take the layout only for searches touching at most kMaxLtTable block B-1 values (4 MB)
 static constexpr uint32_t kMaxLtLoop = 1024;
-static constexpr uint64_t kMaxLtTable = 65536;
+static constexpr uint64_t kMaxLtTable = GPUHASH_LANETABLE_MAX;
 
 // Plans [lower, upper] (inclusive, lower <= upper) of `msg`.  `rchunk_max` caps the r
 // values per work item (0 = default).  Appends to `out`.

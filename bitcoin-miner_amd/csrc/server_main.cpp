@@ -120,13 +120,14 @@ class Scheduler {
         if (m.data.size() > GPUHASH_MAX_MSG)
             return "Data is " + std::to_string(m.data.size()) + " bytes, over the engine's limit";
         // every job cut from it must fit one LSP datagram (2000-byte reads, lspnet/conn.go:35):
-        // a job's bounds can have 20 digits where the client sent Lower = 0, and a truncated
-        // datagram is never acked, so the job would hang (bitcoin/server.py request_error)
+        // a job's bounds can have more digits than the client's Lower (but never exceed its
+        // Upper), and a truncated datagram is never acked, so the job would hang
+        // (bitcoin/server.py request_error)
         {
             BtcMsg job;
             job.type = lspn::Request;
             job.data = m.data;
-            job.lower = job.upper = lspn::kU64Max;
+            job.lower = job.upper = m.upper;
             const std::string frame =
                 lspn::lsp_marshal(lspn::LspMsg{lspn::MsgData, 2147483647, 2147483647, true, lspn::btc_marshal(job)});
             if (frame.size() > lspn::kMaxDatagram)

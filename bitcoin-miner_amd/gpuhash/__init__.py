@@ -89,7 +89,10 @@ class Stats(ctypes.Structure):
 
 
 class LaunchRecord(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_int32) for n in ("device", "J", "C2", "EX", "digits", "c")] + [
+    """gpuhash_launch_record (include/gpuhash.h)."""
+    _fields_ = [(n, ctypes.c_int32) for n in ("device", "J", "C2", "EX", "digits", "c", "shard",
+                                               "stream_device")] + [
+        ("lo", ctypes.c_uint64), ("hi", ctypes.c_uint64),
         ("nonces", ctypes.c_uint64), ("ms", ctypes.c_double), ("sclk_mhz", ctypes.c_double)]
 
     def as_dict(self) -> dict:

@@ -71,13 +71,20 @@ typedef struct gpuhash_stats {
 /* One scan-kernel launch of the last call (bench.py derives the dominant kernel's
  * average launch time and algorithmic work from these). */
 typedef struct gpuhash_launch_record {
-    int32_t device;   /* HIP ordinal                                                */
+    int32_t device;   /* HIP ordinal of the context entry that ran the launch       */
     int32_t J;        /* kernel variant: loop-word index in the final block (0..15) */
-    int32_t C2;       /* 1: lane digits spill into the previous block; 2: and the   */
-                      /*    last block's W_0/W_1 are loop words (uniform schedule)  */
+    int32_t C2;       /* 1: lane digits spill into block B-1, per-nonce schedule;   */
+                      /* 2: block B's W_0/W_1 hold only loop digits, schedules      */
+                      /*    shared per wave through LDS; 3: lane table (per-lane    */
+                      /*    block-B schedule, block B-1 state from a p-table)       */
     int32_t EX;       /* 1: extra all-constant padding block                        */
     int32_t digits;   /* decimal digits of every nonce in the launch                */
     int32_t c;        /* 64-byte blocks holding nonce digits (1 or 2)               */
+    int32_t shard;    /* index of the context entry (gpuhash_open's list position)  */
+    int32_t stream_device; /* ordinal the HIP runtime reports for the stream the    */
+                      /*    kernel was launched on (hipStreamGetDevice): evidence   */
+                      /*    that the shard ran on `device`, not on device 0         */
+    uint64_t lo, hi;  /* the shard's inclusive nonce range in this slice            */
     uint64_t nonces;  /* nonces covered by the launch                               */
     double ms;        /* HIP-event time of the launch on the device's stream        */
     double sclk_mhz;  /* shader clock over the launch, measured in the kernel:      */
@@ -111,18 +118,28 @@ int gpuhash_device_count(void);
 int gpuhash_shard_range(size_t msg_len, uint64_t lower, uint64_t upper, int nshards,
                         uint64_t *out_lower, uint64_t *out_upper);
 
-/* Layout choice for nonces whose digits straddle two SHA blocks with 5-8 digits in the
- * last one: AUTO (default) takes the uniform-schedule layout (C2 = 2)
- * when the search fills its lane rows and the lane-table layout (C2 = 3) otherwise;
- * UNIFORM takes C2 = 2 whenever block B-1 holds >= 3 digits, else C2 = 3; CLASSIC always
- * the per-nonce-schedule layout (C2 = 1); LANETABLE always C2 = 3.  Results are
- * identical under every policy; only speed differs.  Exposed for tuning and so that
- * parity tests can drive every kernel over small ranges.  Replaces nothing in the
- * reference. */
+/* Layout choice for a digit group whose digits straddle two SHA blocks with the loop word
+ * at W_1 of the last block, i.e. 5-8 digits in the last block.  Let
+ * q = the digits in block B's W_0/W_1 (RQ = 10^q nonces per block B-1 value), nb1 = the
+ * digits in block B-1, span = the search's nonces in that digit group, and N =
+ * (span - 1) / RQ + 2, the block B-1 values such a span can touch.  This comment is
+ * the ONE statement of the rule; csrc/plan.cpp (layout_for) implements it and
+ * tests/test_plan.py checks the two against each other.
+ *   AUTO (default)  span < 2 * RQ                                -> C2 = 1 (classic)
+ *                   else nb1 >= 3 and N > GPUHASH_LANETABLE_MAX  -> C2 = 2 (two-word loop)
+ *                   else                                         -> C2 = 3 (lane table)
+ *   UNIFORM         nb1 >= 3 -> C2 = 2, else C2 = 3
+ *   CLASSIC         C2 = 1 always (the per-nonce-schedule layout)
+ *   LANETABLE       C2 = 3 up to N = GPUHASH_LANETABLE_MAX, C2 = 2 beyond it (each value
+ *                   costs 64 B of table and one compression, so the cap bounds memory)
+ * Results are identical under every policy; only speed differs.  Exposed for tuning and
+ * so that parity tests can drive every kernel over small ranges.  Replaces nothing in
+ * the reference. */
 #define GPUHASH_LAYOUT_AUTO 0
 #define GPUHASH_LAYOUT_UNIFORM 1
 #define GPUHASH_LAYOUT_CLASSIC 2
 #define GPUHASH_LAYOUT_LANETABLE 3
+#define GPUHASH_LANETABLE_MAX 65536u
 int gpuhash_set_layout_policy(gpuhash_ctx *ctx, int policy);
 
 /* argmin_{n in [lower, upper]} (Hash(msg, n), n) -> *out_hash, *out_nonce.

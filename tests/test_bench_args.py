@@ -75,3 +75,66 @@ def test_roofline_of_the_dominant_kernel(monkeypatch):
     assert r["achieved"] == pytest.approx(want, rel=1e-3)
     assert r["frac"] == pytest.approx(want / bench.VALU_PEAK_T, rel=1e-3)
     assert r["traffic"] is None and r["issued_frac"] is None
+
+
+# ---- the 2^40 search leg ----
+
+def _srec(shard, dev, lo, hi, ms, stream_dev=None, J=4):
+    return {"device": dev, "shard": shard, "stream_device": dev if stream_dev is None else stream_dev,
+            "J": J, "C2": 0, "EX": 0, "digits": 10, "c": 1, "lo": lo, "hi": hi,
+            "nonces": hi - lo + 1, "ms": ms, "sclk_mhz": 2400.0}
+
+
+def test_search_range_parsing():
+    assert bench.parse_search("0:2^40-1") == (0, (1 << 40) - 1)
+    assert bench.parse_search("5:4294967295") == (5, (1 << 32) - 1)
+    assert bench.parse_search("off") is None
+    for bad in ("9:3", "0:2^64", "-1:5"):
+        with pytest.raises(ValueError):
+            bench.parse_search(bad)
+    r = _run(["--search", "9:3"])
+    assert r.returncode == 2 and "LO <= HI" in r.stderr
+
+
+def test_search_golden_is_the_committed_2p40_fixture():
+    """The default search range is exactly config 4's golden range, so every bench line's
+    search_2p40 is checked against oracle/golden_scan.c's [0, 2^40) result."""
+    want, name = bench.golden_for(bench.MSG, *bench.SEARCH_DEFAULT)
+    assert name == "cfg4_bradfitz_2p40" and want == (16555811, 890536971553)
+    assert bench.golden_for(bench.MSG, 0, (1 << 32) - 1)[1] == "cfg2_bradfitz_2p32"
+    assert bench.golden_for(b"nope", 0, 1) == (None, None)
+    line = bench.search_line((16555811, 890536971553), 4.0, 8, *bench.SEARCH_DEFAULT, "inproc",
+                             list(range(8)), [])
+    assert line["matches_golden"] is True and line["GHs"] == pytest.approx((1 << 40) / 4e9, rel=1e-4)
+    assert line["per_gpu_GHs"] == pytest.approx(line["GHs"] / 8, rel=1e-3)
+    bad = bench.search_line((16555811, 890536971554), 4.0, 8, *bench.SEARCH_DEFAULT, "inproc", [0], [])
+    assert bad["matches_golden"] is False
+    with pytest.raises(SystemExit) as e:
+        bench.search_exit({"search_2p40": bad}, [])
+    assert e.value.code == 3
+
+
+def test_shard_rows_and_device_checks():
+    # 2 shards on devices 3 and 5, two slices each, two kernel groups in the second slice
+    recs = [_srec(0, 3, 0, 99, 1.0), _srec(1, 5, 100, 199, 1.5),
+            _srec(0, 3, 200, 299, 1.0), _srec(0, 3, 200, 299, 0.5, J=3), _srec(1, 5, 300, 399, 1.0)]
+    rows = bench.shard_rows(recs)
+    assert [(r["shard"], r["device"], r["lo"], r["hi"], r["slices"], r["nonces"]) for r in rows] == \
+        [(0, 3, 0, 299, 2, 200), (1, 5, 100, 399, 2, 200)]
+    assert rows[0]["kernel_ms"] == pytest.approx(2.5)
+    assert bench.check_shards(rows, [3, 5]) == []
+    assert bench.check_shards(rows, [5, 3])  # shard 0 did not run on the listed device
+    # a stream the runtime placed on another device is caught
+    rows2 = bench.shard_rows([_srec(0, 3, 0, 9, 1.0, stream_dev=0), _srec(1, 5, 10, 19, 1.0)])
+    assert any("stream" in p for p in bench.check_shards(rows2, [3, 5]))
+    # distinct devices requested, but two shards report the same one
+    rows3 = bench.shard_rows([_srec(0, 3, 0, 9, 1.0), _srec(1, 3, 10, 19, 1.0)])
+    assert bench.check_shards(rows3, [3, 3]) == []  # a rehearsal on one GPU: allowed
+    assert any("share" in p for p in bench.check_shards(rows3, [3, 4]))
+
+
+def test_host_cpus_reports_the_usable_share():
+    h = bench.host_cpus()
+    assert h["nproc"] >= h["affinity"] >= h["usable"] >= 1
+    if h["cgroup_quota_cpus"] is not None:
+        assert h["usable"] <= max(1, int(h["cgroup_quota_cpus"]))

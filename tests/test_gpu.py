@@ -333,7 +333,48 @@ def test_multi_device_sharding_and_host_argmin(engine, oracle):
             assert multi.min(m, lo, hi) == engine.min(m, lo, hi)
         st = multi.stats()
         assert st["ndevices"] == 3 and st["launches"] >= 3
+        # the launch records name their shard and the stream's runtime device
+        recs = multi.launches()
+        assert {r["shard"] for r in recs} == {0, 1, 2}
+        assert all(r["device"] == 0 and r["stream_device"] == 0 for r in recs)
         assert multi.min(b"bradfitz", 0, 9999) == oracle.min(b"bradfitz", 0, 9999)
+
+
+def _check_distinct_shards(recs, devs, lo, hi):
+    """Every launch ran on the device its shard names (record ordinal == the context's
+    entry, the stream's runtime ordinal == that device), and the shards tile [lo, hi]."""
+    for r in recs:
+        assert r["device"] == devs[r["shard"]] and r["stream_device"] == r["device"], r
+    wins = sorted({(r["lo"], r["hi"], r["shard"]) for r in recs})
+    assert wins[0][0] == lo and wins[-1][1] == hi
+    assert all(b[0] == a[1] + 1 for a, b in zip(wins, wins[1:]))
+    assert [w[2] for w in wins] == sorted(w[2] for w in wins)  # shard k < shard k+1 in range order
+
+
+def test_distinct_devices(oracle, golden):
+    """the multi-device path with DISTINCT ordinals -- every visible
+    GPU in one context.  A bug that only shows with distinct devices (a buffer, stream or
+    event on the wrong device, occupancy queried on another ordinal) cannot surface in the
+    repeated-ordinal tests above.  Runs wherever >= 2 GPUs are visible; skips on one."""
+    import gpuhash
+    n = gpuhash.device_count()
+    if n < 2:
+        pytest.skip(f"{n} HIP device visible: distinct-device sharding needs >= 2 "
+                    "(repeated-ordinal rehearsals: test_multi_device_sharding_and_host_argmin)")
+    devs = list(range(n))
+    with gpuhash.Engine(devs) as multi:
+        # a 1 -> 2 SHA block straddle (m = 45 at 9 -> 10 digits), against the oracle
+        m, lo, hi = M120[:45], 10 ** 9 - (1 << 22), 10 ** 9 + (1 << 22)
+        assert multi.min(m, lo, hi) == oracle.min(m, lo, hi, threads=8)
+        _check_distinct_shards(multi.launches(), devs, lo, hi)
+        # a whole config-5 request [0, 2^36] split over every device, against its CPU golden
+        g = next(r for r in golden["ranges"] if r["name"] == "cfg5_client-00_2p36")
+        got = multi.min(bytes.fromhex(g["msg_hex"]), g["lower"], g["upper"])
+        assert got == (g["hash"], g["nonce"])
+        recs = multi.launches()
+        _check_distinct_shards(recs, devs, g["lower"], g["upper"])
+        assert {r["device"] for r in recs} == set(devs)  # every GPU took a shard
+        assert multi.stats()["ndevices"] == n
 
 
 def test_more_shards_than_nonces(oracle):

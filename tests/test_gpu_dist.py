@@ -85,7 +85,10 @@ def _bench(args, env_extra=None, launcher=None, timeout=100):
 
 
 def test_bench_inproc_two_shards_on_one_gpu(engine):
-    r = _bench(["--inproc", "0,0", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"])
+    """bench.py's in-process N=2 path rehearsed as two shards on the one GPU, INCLUDING the
+    default search leg: config 4's whole [0, 2^40) of 'bradfitz' in one gpuhash_min over
+    the two shards, checked by bench.py against the committed CPU golden."""
+    r = _bench(["--inproc", "0,0", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"], timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "inproc2"
@@ -93,6 +96,15 @@ def test_bench_inproc_two_shards_on_one_gpu(engine):
     assert tuple(line["result"]) == engine.min(b"bradfitz", 0, (2 << 32) - 1)
     assert line["roofline"]["kernel"] == "k_scan<J=4,C2=0,EX=0,MODE=0>"
     assert len(line["per_device"]) == 1  # both shards report device ordinal 0
+    assert [s["shard"] for s in line["shards"]] == [0, 1] and "device_check" not in line
+    s = line["search_2p40"]
+    assert s["range"] == [0, (1 << 40) - 1] and s["golden_name"] == "cfg4_bradfitz_2p40"
+    assert s["matches_golden"] is True and tuple(s["result"]) == (16555811, 890536971553)
+    # two shards tile [0, 2^40) in order, each on the stream of the device it names
+    sh = s["shards"]
+    assert [x["shard"] for x in sh] == [0, 1] and sh[0]["lo"] == 0 and sh[1]["hi"] == (1 << 40) - 1
+    assert sh[1]["lo"] == sh[0]["hi"] + 1 and sum(x["nonces"] for x in sh) == 1 << 40
+    assert all(x["device"] == 0 and x["stream_device"] == [0] for x in sh)
 
 
 def test_bench_gpus_above_visible_fails_loudly():
@@ -107,7 +119,8 @@ def test_bench_torchrun_two_ranks_on_one_gpu(engine):
     port = _free_port()
     launcher = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                 "--master-addr", "127.0.0.1", "--master-port", str(port)]
-    r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"],
+    r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu-baseline",
+                "--search", "0:4294967295"],
                {"GPUHASH_SHARE_GPU": "1"}, launcher=launcher)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
@@ -115,6 +128,12 @@ def test_bench_torchrun_two_ranks_on_one_gpu(engine):
     assert line["config"]["backend"] == "gloo"
     # rank r searched [r*2^32, (r+1)*2^32): the merged result is the whole range's argmin
     assert tuple(line["result"]) == engine.min(b"bradfitz", 0, (2 << 32) - 1)
+    # the search leg: each rank its cost-balanced window of config 2's range, gloo merge,
+    # checked against the committed golden (5256245051, 1626825724)
+    s = line["search_2p40"]
+    assert s["golden_name"] == "cfg2_bradfitz_2p32" and s["matches_golden"] is True
+    assert [x["shard"] for x in s["shards"]] == [0, 1] and s["devices"] == [0, 0]
+    assert s["shards"][1]["lo"] == s["shards"][0]["hi"] + 1 and "device_check" not in line
     # without GPUHASH_SHARE_GPU, a second rank on a 1-GPU box is refused
     import gpuhash
     if gpuhash.device_count() == 1:

@@ -1,0 +1,119 @@
+"""CPU: the two Go-compatible JSON readers -- bitcoin.unmarshal (Python server/miner) and
+csrc/lsp_native.h btc_unmarshal (compiled server/miner) -- decode every document of a
+corpus the way Go's json.Unmarshal into bitcoin.Message (message.go:16-21) does, and so
+agree with each other byte for byte (invalid UTF-8 one U+FFFD per byte,
+malformed nested values rejected, duplicate keys with null / wrong-type members)."""
+import os
+import subprocess
+
+import pytest
+
+import bitcoin
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+U64 = (1 << 64) - 1
+F = "�".encode()
+
+# (document, expected) -- expected None: Go's Unmarshal returns an error (message dropped);
+# else (Type, Data bytes, Lower, Upper)
+CASES = [
+    (b'{"Type":1,"Data":"x","Lower":1,"Upper":2}', (1, b"x", 1, 2)),
+    # invalid UTF-8 inside the string: one U+FFFD per invalid byte (utf8.DecodeRune size 1)
+    (b'{"Type":1,"Data":"\xe2\x82A","Upper":2}', (1, F + F + b"A", 0, 2)),
+    (b'{"Type":1,"Data":"\xf0\x9f\x98","Upper":2}', (1, F * 3, 0, 2)),
+    (b'{"Type":1,"Data":"\xf0\x9f\x98\x80","Upper":2}', (1, b"\xf0\x9f\x98\x80", 0, 2)),
+    (b'{"Type":1,"Data":"\xed\xa0\x80","Upper":2}', (1, F * 3, 0, 2)),   # encoded surrogate
+    (b'{"Type":1,"Data":"\xc0\x80z","Upper":2}', (1, F * 2 + b"z", 0, 2)),  # overlong NUL
+    (b'{"Type":1,"Data":"\xff\xfe","Upper":2}', (1, F * 2, 0, 2)),
+    (b'{"Type":1,"Data":"\x80\xbf","Upper":2}', (1, F * 2, 0, 2)),  # stray continuations
+    (b'{"Type":1,"Data":"\xf4\x90\x80\x80","Upper":2}', (1, F * 4, 0, 2)),  # > U+10FFFF
+    # malformed nested values in an unknown field: the whole document is a syntax error
+    (b'{"Type":1,"X":[1 2],"Upper":2}', None),
+    (b'{"Type":1,"X":{1:2},"Upper":2}', None),
+    (b'{"Type":1,"X":{"a"},"Upper":2}', None),
+    (b'{"Type":1,"X":[,,],"Upper":2}', None),
+    (b'{"Type":1,"X":[1,],"Upper":2}', None),
+    (b'{"Type":1,"X":{"a":1,},"Upper":2}', None),
+    (b'{"Type":1,"X":[1]],"Upper":2}', None),
+    (b'{"Type":1,"X":{"a":[1,{"b":"}]"}],"c":null},"Upper":2}', (1, b"", 0, 2)),
+    (b'{"Type":1,"X":[],"Y":{},"Upper":2}', (1, b"", 0, 2)),
+    # numbers: RFC 8259 grammar (Go's scanner), uint64 fields ParseUint
+    (b'{"Type":1,"X":1-2,"Upper":2}', None),
+    (b'{"Type":1,"X":01,"Upper":2}', None),
+    (b'{"Type":1,"X":-,"Upper":2}', None),
+    (b'{"Type":1,"X":1.,"Upper":2}', None),
+    (b'{"Type":1,"X":1e,"Upper":2}', None),
+    (b'{"Type":1,"X":-0.5e+7,"Upper":2}', (1, b"", 0, 2)),
+    (b'{"Type":1,"X":NaN,"Upper":2}', None),
+    (b'{"Type":1,"X":-Infinity,"Upper":2}', None),
+    (b'{"Type":1,"Upper":1e3}', None),
+    (b'{"Type":1,"Upper":-0}', None),
+    (b'{"Type":1,"Upper":18446744073709551615}', (1, b"", 0, U64)),
+    (b'{"Type":1,"Upper":18446744073709551616}', None),
+    (b'{"Type":-0,"Upper":3}', (0, b"", 0, 3)),
+    # duplicate keys (any ASCII case): every member decodes in order; null leaves the
+    # field as it was; one member of the wrong type fails the message
+    (b'{"Type":1,"Lower":5,"lower":null,"Upper":9}', (1, b"", 5, 9)),
+    (b'{"Type":1,"Lower":"x","Lower":1,"Upper":9}', None),
+    (b'{"Type":1,"Lower":1,"LOWER":true,"Upper":9}', None),
+    (b'{"Type":1,"Data":"a","data":null,"Upper":9}', (1, b"a", 0, 9)),
+    (b'{"Type":1,"Data":"a","DATA":"b","Upper":9}', (1, b"b", 0, 9)),
+    (b'{"Type":1,"Data":5,"data":"b","Upper":9}', None),
+    (b'{"Type":null,"type":1,"Upper":9,"upper":null}', (1, b"", 0, 9)),
+    (b'{"Type":1,"Upper":9,"upper":7}', (1, b"", 0, 7)),
+]
+
+
+@pytest.fixture(scope="module")
+def probe(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("json") / "json_probe")
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-I",
+                           os.path.join(ROOT, "bitcoin-miner_amd", "csrc"), "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "json_probe.cpp"), "-lpthread", "-o", exe])
+    return exe
+
+
+def _native(exe, docs):
+    out = subprocess.run([exe], input="\n".join(d.hex() for d in docs) + "\n", capture_output=True,
+                         text=True, timeout=30, check=True).stdout.splitlines()
+    res = []
+    for ln in out:
+        if ln == "ERR":
+            res.append(None)
+        else:
+            _, t, lo, up, _h, _n, *data = ln.split(" ")
+            res.append((int(t), bytes.fromhex(data[0] if data else ""), int(lo), int(up)))
+    return res
+
+
+def _python(doc):
+    try:
+        m = bitcoin.unmarshal(doc)
+    except (ValueError, TypeError):
+        return None
+    return (int(m.Type), m.Data.encode(), m.Lower, m.Upper)
+
+
+def test_python_reader_decodes_like_go():
+    for doc, want in CASES:
+        assert _python(doc) == want, doc
+
+
+def test_native_reader_decodes_like_go(probe):
+    got = _native(probe, [d for d, _ in CASES])
+    for (doc, want), g in zip(CASES, got):
+        assert g == want, doc
+
+
+def test_readers_agree_on_random_byte_strings(probe):
+    """Random Data payloads of raw bytes (any UTF-8 validity) inside a Request: the two
+    readers produce the same Data bytes, hence hash the same message."""
+    import random
+    rng = random.Random(7)
+    docs = []
+    for _ in range(400):
+        n = rng.randrange(0, 24)
+        raw = bytes(rng.choice([rng.randrange(0x80, 0x100), rng.randrange(0x20, 0x7F)]) for _ in range(n))
+        raw = raw.replace(b'"', b"'").replace(b"\\", b"/")
+        docs.append(b'{"Type":1,"Data":"' + raw + b'","Lower":0,"Upper":7}')
+    assert _native(probe, docs) == [_python(d) for d in docs]

@@ -260,12 +260,13 @@ def test_a_small_request_is_not_starved_by_a_large_one(procs, plain_server, mine
     assert "dropped request" in s.log()
 
 
-def _longest_servable_data():
-    """Largest ASCII Data whose worst-case job frame still fits one LSP datagram."""
+def _longest_servable_data(upper):
+    """Largest ASCII Data whose worst-case job frame (both bounds at `upper`) still fits
+    one LSP datagram."""
     import lspnet
     from bitcoin.server import job_frame_worst_case
     n = 1000
-    while len(job_frame_worst_case("d" * (n + 1))) <= lspnet.MAX_DATAGRAM:
+    while len(job_frame_worst_case("d" * (n + 1), upper)) <= lspnet.MAX_DATAGRAM:
         n += 1
     return n
 
@@ -277,7 +278,11 @@ def test_jobs_must_fit_one_datagram_python_and_compiled(procs, plain_server, min
     longest one whose jobs fit, end to end."""
     import lspnet
     from bitcoin.server import request_error
-    n = _longest_servable_data()
+    n = _longest_servable_data(99)
+    # ADVICE r03: jobs are priced at the request's Upper, not at 2^64-1 -- a 2-digit Upper
+    # leaves room for 36 more bytes of Data than a 20-digit one
+    assert n == _longest_servable_data(bitcoin.UINT64_MAX) + 36
+    assert request_error("d" * n, 0, 99) is None and "datagram" in request_error("d" * n, 0, bitcoin.UINT64_MAX)
     client_frame = lsp.message.NewData(1, 1, bitcoin.marshal(bitcoin.NewRequest("d" * (n + 1), 0, 99))).marshal()
     assert len(client_frame) <= lspnet.MAX_DATAGRAM  # the client's own Request fits
     assert request_error("d" * n, 0, 99) is None

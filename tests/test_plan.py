@@ -123,25 +123,50 @@ def test_descriptor_replay_matches_oracle(hc, oracle, policy):
     assert len(seen - straddle) == 18, sorted(seen)
 
 
+def _header_rule():
+    """The layout-policy rule as include/gpuhash.h states it (the ONE statement of it,
+    VERDICT r03 item 4): GPUHASH_LANETABLE_MAX and the four policy lines."""
+    import re
+    h = open(os.path.join(ROOT, "include", "gpuhash.h")).read()
+    cap = int(re.search(r"#define GPUHASH_LANETABLE_MAX (\d+)u", h).group(1))
+    block = h[h.index("Layout choice for a digit group"):h.index("#define GPUHASH_LAYOUT_AUTO")]
+    rule = " ".join(" ".join(re.sub(r"^\s*\*\s?", "", ln) for ln in block.splitlines()).split())
+    return cap, rule
+
+
 def test_layout_policy_for_straddling_j1(hc):
-    """J = 1 straddles (4 + q1 digits in block B's W_0/W_1, the rest in block B-1).  AUTO
-    takes the lane table (C2 = 3) unless the search touches more than 65536 block B-1
-    values, then the two-word uniform loop (C2 = 2), whose rows are full there, or spans
-    fewer than 2 block B-1 values, then the classic layout (C2 = 1); CLASSIC
-    always C2 = 1, LANETABLE always C2 = 3, UNIFORM C2 = 2 whenever block B-1 holds >= 3
-    digits (round 2's rule)."""
+    """J = 1 straddles (4 + q1 digits in block B's W_0/W_1, the rest in block B-1), checked
+    against the rule include/gpuhash.h states: AUTO takes the classic layout (C2 = 1) when
+    span < 2 * RQ, the two-word loop (C2 = 2) when block B-1 holds >= 3 digits and
+    N = (span - 1) / RQ + 2 > GPUHASH_LANETABLE_MAX, else the lane table (C2 = 3); UNIFORM
+    C2 = 2 whenever block B-1 holds >= 3 digits; CLASSIC C2 = 1; LANETABLE C2 = 3 up to
+    the same cap, C2 = 2 beyond it (uncapped, a wide LANETABLE search asked
+    for ~640 MB of p-table)."""
+    cap, rule = _header_rule()
+    assert cap == 65536
+    for line in ("AUTO (default) span < 2 * RQ -> C2 = 1 (classic)",
+                 "else nb1 >= 3 and N > GPUHASH_LANETABLE_MAX -> C2 = 2 (two-word loop)",
+                 "else -> C2 = 3 (lane table)",
+                 "UNIFORM nb1 >= 3 -> C2 = 2, else C2 = 3",
+                 "CLASSIC C2 = 1 always",
+                 "LANETABLE C2 = 3 up to N = GPUHASH_LANETABLE_MAX, C2 = 2 beyond it",
+                 "N = (span - 1) / RQ + 2"):
+        assert line in rule, line
     pick = lambda m, a, b: {(l.J, l.C2) for l in plan(hc, m, a, b)}
     # m = 59, d = 12: 4 digits in block 0, 8 in block 1 (RQ = 10^8): at most 9000 values
     m = b"y" * 59
     lo = 10 ** 11
     narrow, wide = (lo, lo + 10 ** 9), (lo, lo + 5 * 10 ** 11)
     assert pick(m, *narrow) == {(1, 3)} and pick(m, *wide) == {(1, 3)}
-    # m = 56, d = 12: 7 digits in block 0, 5 in block 1 (RQ = 10^5)
-    m56 = b"z" * 56
-    assert pick(m56, lo, lo + 65000 * 10 ** 5) == {(1, 3)}
-    assert pick(m56, lo, lo + 70000 * 10 ** 5) == {(1, 2)}
+    # m = 56, d = 12: 7 digits in block 0 (nb1 = 7), 5 in block 1 (RQ = 10^5); the cap's
+    # edge: N = cap -> lane table, N = cap + 1 -> two-word loop
+    m56, RQ = b"z" * 56, 10 ** 5
+    at_cap = lo + (cap - 1) * RQ - 1  # span - 1 = (cap - 1) * RQ - 1 -> N = cap
+    assert pick(m56, lo, at_cap) == {(1, 3)}
+    assert pick(m56, lo, at_cap + 1) == {(1, 2)}
     # fewer than 2 block B-1 values' worth of nonces: the classic layout
     assert pick(m, lo, lo + 10 ** 8) == {(1, 1)} and pick(m, lo, lo + 2 * 10 ** 8) == {(1, 3)}
+    assert pick(m, lo, lo + 2 * 10 ** 8 - 2) == {(1, 1)}  # span = 2 * RQ - 1
     try:
         hc.hostcheck_set_layout_policy(UNIFORM)
         assert pick(m, *narrow) == {(1, 2)}
@@ -149,7 +174,11 @@ def test_layout_policy_for_straddling_j1(hc):
         hc.hostcheck_set_layout_policy(CLASSIC)
         assert pick(m, *wide) == {(1, 1)} and pick(m, *narrow) == {(1, 1)}
         hc.hostcheck_set_layout_policy(LANETABLE)
-        assert pick(m, *wide) == {(1, 3)} and pick(m56, lo, lo + 70000 * 10 ** 5) == {(1, 3)}
+        assert pick(m, *wide) == {(1, 3)} and pick(m, lo, lo + 10 ** 8) == {(1, 3)}
+        assert pick(m56, lo, at_cap) == {(1, 3)} and pick(m56, lo, at_cap + 1) == {(1, 2)}
+        # ADVICE r03's example: q = 5 over 10^12 nonces stays bounded (C2 = 2, not a
+        # 10^7-entry p-table)
+        assert pick(m56, lo, lo + 10 ** 12) == {(1, 2)}
     finally:
         hc.hostcheck_set_layout_policy(AUTO)
 

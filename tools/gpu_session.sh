@@ -2,7 +2,7 @@
 # tools/gpu_session.sh STEP... -- runs GPU steps on the gpurun box, each under its own
 # time limit, logging to gpurun_out/.  A plain failure (exit 1, e.g. a failing test)
 # lets the next step run; a fault, abort, segfault, time limit or kill stops the session.
-# Steps: cumask | family | inproc8c4 | valu | go | test | soak | smoke | bench | bench3 | bench4 | prof4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | pmc3 | pmc4 | sweep | variants | partial | regret | sys5
+# Steps: fma | cumask | family | inproc8c4 | valu | go | test | soak | smoke | bench | bench3 | bench4 | prof4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | pmc3 | pmc4 | sweep | variants | partial | regret | sys5
 set -u
 cd "$(dirname "$0")/.."
 OUT=gpurun_out
@@ -28,6 +28,7 @@ run() {  # run <name> <seconds> <cmd...>
 
 for step in "$@"; do
     case $step in
+        fma) run fma 180 ./tools/bin/fma_probe 20000 ;;
         valu) run valu 120 ./tools/bin/valu_peak 8 50000; run valu1 120 ./tools/bin/valu_peak 1 50000 ;;
         probe) run probe8 300 ./tools/bin/valu_probe 8 20000 ;;
         listctr) run listctr 120 rocprofv3 -L ;;
@@ -37,6 +38,7 @@ for step in "$@"; do
         systest) run pytest_sys 600 python -u -m pytest tests/test_gpu_system.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 300 python -u bench.py --steps 10 --warmup 2 ;;
+        inproc40) run inproc40 300 python -u bench.py --inproc 0,0 --steps 2 --warmup 1 --no-cpu-baseline ;;
         nccl1) run nccl1 300 env GPUHASH_FORCE_DIST=1 GPUHASH_DIST_BACKEND=nccl python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29541 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
         dist2) run dist2 300 env GPUHASH_SHARE_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 ;;
         inproc) run inproc2 300 python -u bench.py --inproc 0,0 --steps 3 --warmup 1 --no-cpu-baseline ;;
@@ -62,19 +64,19 @@ for step in "$@"; do
         dist8c4) run dist8c4 400 env GPUHASH_SHARE_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29547 bench.py --gpus 8 --config 4 --steps 1 --warmup 0 ;;
         bench3) run bench3 300 python -u bench.py --config 3 --steps 5 --warmup 1 ;;
         bench4) run bench4 300 python -u bench.py --config 4 --steps 2 --warmup 1 ;;
-        prof4) run prof_c4 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c4" -o bench --output-format csv -- python3 bench.py --config 4 --steps 1 --warmup 1 --no-cpu-baseline ;;
-        prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
-        pmc) run pmc_valu 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/pmc1" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
-             run pmc_derived 120 rocprofv3 --pmc VALUBusy VALUUtilization -d "$OUT/pmc4" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
-             run pmc_hbm 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc2" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
-             run pmc_wr 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc3" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
-        pmc3) B3="python3 bench.py --config 3 --steps 2 --warmup 1 --no-cpu-baseline"
+        prof4) run prof_c4 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c4" -o bench --output-format csv -- python3 bench.py --config 4 --steps 1 --warmup 1 --no-cpu-baseline --no-search ;;
+        prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-search ;;
+        pmc) run pmc_valu 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/pmc1" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-search
+             run pmc_derived 120 rocprofv3 --pmc VALUBusy VALUUtilization -d "$OUT/pmc4" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-search
+             run pmc_hbm 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc2" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-search
+             run pmc_wr 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc3" -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-search ;;
+        pmc3) B3="python3 bench.py --config 3 --steps 2 --warmup 1 --no-cpu-baseline --no-search"
               run prof_c3 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c3" -o bench --output-format csv -- $B3
               run pmc_valu_c3 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/pmc1_c3" -o pmc --output-format csv -- $B3
               run pmc_derived_c3 120 rocprofv3 --pmc VALUBusy VALUUtilization -d "$OUT/pmc4_c3" -o pmc --output-format csv -- $B3
               run pmc_hbm_c3 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc2_c3" -o pmc --output-format csv -- $B3
               run pmc_wr_c3 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc3_c3" -o pmc --output-format csv -- $B3 ;;
-        pmc4) B4="python3 bench.py --config 4 --steps 1 --warmup 1 --no-cpu-baseline"
+        pmc4) B4="python3 bench.py --config 4 --steps 1 --warmup 1 --no-cpu-baseline --no-search"
               run prof_c4 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c4" -o bench --output-format csv -- $B4
               run pmc_valu_c4 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/pmc1_c4" -o pmc --output-format csv -- $B4
               run pmc_derived_c4 120 rocprofv3 --pmc VALUBusy VALUUtilization -d "$OUT/pmc4_c4" -o pmc --output-format csv -- $B4
