@@ -403,8 +403,9 @@ def golden_for(msg: bytes, lo: int, hi: int):
 def shard_rows(recs: list[dict]) -> list[dict]:
     """Per shard (position in the context's device list) of one gpuhash_min call: its HIP
     ordinal, the ordinal the runtime reports for its stream, the nonce windows it searched
-    (one per slice), its scan-kernel time and rate.  Every record of one slice of a shard
-    carries that slice's [lo, hi]."""
+    (one per slice: a search longer than 2^38 nonces per device runs as slices, each cut
+    over every shard, so a shard's windows interleave with the others'), its scan-kernel
+    time and rate.  Every record of one slice of a shard carries that slice's [lo, hi]."""
     by = {}
     for r in recs:
         e = by.setdefault(r["shard"], {"shard": r["shard"], "device": r["device"],
@@ -418,17 +419,24 @@ def shard_rows(recs: list[dict]) -> list[dict]:
         wins = sorted(e["windows"])
         nonces = sum(b - a + 1 for a, b in wins)
         rows.append({"shard": k, "device": e["device"], "stream_device": sorted(e["stream_devices"]),
-                     "lo": wins[0][0], "hi": wins[-1][1], "slices": len(wins), "nonces": nonces,
+                     "windows": [list(w) for w in wins], "slices": len(wins), "nonces": nonces,
                      "kernel_ms": round(e["kernel_ms"], 3),
                      "kernel_GHs": round(nonces / (e["kernel_ms"] * 1e-3) / 1e9, 4) if e["kernel_ms"] else None})
     return rows
 
 
+def tiles(rows: list[dict], lo: int, hi: int) -> bool:
+    """The shards' windows, all slices together, cover [lo, hi] exactly once."""
+    wins = sorted(tuple(w) for r in rows for w in r["windows"])
+    return bool(wins) and wins[0][0] == lo and wins[-1][1] == hi and all(
+        b[0] == a[1] + 1 for a, b in zip(wins, wins[1:]))
+
+
 def check_shards(rows: list[dict], devs: list[int]) -> list[str]:
     """Device evidence of a search's shards: shard k ran on devs[k] (the record's ordinal and
-    the stream's runtime ordinal agree with it), the shards' windows tile the search in
-    order, and -- when the device list has no repeats -- every shard ran on a different
-    device.  Returns the problems found (empty = fine)."""
+    the stream's runtime ordinal agree with it), and -- when the device list has no
+    repeats -- every shard ran on a different device.  Returns the problems found (empty =
+    fine)."""
     bad = []
     for r in rows:
         if r["shard"] >= len(devs) or r["device"] != devs[r["shard"]]:
@@ -541,6 +549,8 @@ def main_inproc(args, devs: list[int]) -> None:
         sdt = time.perf_counter() - t0
         rows = shard_rows(eng.launches())
         problems += check_shards(rows, devs)
+        if not tiles(rows, lo, hi):
+            problems.append("the search's shard windows do not tile its range")
         out["search_2p40"] = search_line(sres, sdt, n, lo, hi, "inproc", devs, rows)
     if problems:
         out["device_check"] = problems
@@ -647,6 +657,8 @@ def main_ranks(args, world: int, rank: int, local: int) -> None:
                                              f"ranks ({backend} merge)", devices, shards)
             if not shared and len({s["device"] for s in shards}) != len(shards):
                 problems.append("ranks on distinct GPUs but search shards share a device")
+            if not tiles(shards, *args.search):
+                problems.append("the ranks' search windows do not tile the range")
         if problems:
             out["device_check"] = problems
         if world == 1:

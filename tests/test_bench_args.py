@@ -119,8 +119,9 @@ def test_shard_rows_and_device_checks():
     recs = [_srec(0, 3, 0, 99, 1.0), _srec(1, 5, 100, 199, 1.5),
             _srec(0, 3, 200, 299, 1.0), _srec(0, 3, 200, 299, 0.5, J=3), _srec(1, 5, 300, 399, 1.0)]
     rows = bench.shard_rows(recs)
-    assert [(r["shard"], r["device"], r["lo"], r["hi"], r["slices"], r["nonces"]) for r in rows] == \
-        [(0, 3, 0, 299, 2, 200), (1, 5, 100, 399, 2, 200)]
+    assert [(r["shard"], r["device"], r["windows"], r["slices"], r["nonces"]) for r in rows] == \
+        [(0, 3, [[0, 99], [200, 299]], 2, 200), (1, 5, [[100, 199], [300, 399]], 2, 200)]
+    assert bench.tiles(rows, 0, 399) and not bench.tiles(rows, 0, 400) and not bench.tiles(rows[:1], 0, 299)
     assert rows[0]["kernel_ms"] == pytest.approx(2.5)
     assert bench.check_shards(rows, [3, 5]) == []
     assert bench.check_shards(rows, [5, 3])  # shard 0 did not run on the listed device

@@ -20,6 +20,7 @@ import torch.multiprocessing as mp
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 M120 = (b"The quick brown fox jumps over the lazy dog. " * 3)[:120]
 # m = 45: 9-digit nonces hash 1 block, 10-digit ones 2 (an extra padding block);
 # m = 50: the same change at 4 -> 5 digits
@@ -100,10 +101,12 @@ def test_bench_inproc_two_shards_on_one_gpu(engine):
     s = line["search_2p40"]
     assert s["range"] == [0, (1 << 40) - 1] and s["golden_name"] == "cfg4_bradfitz_2p40"
     assert s["matches_golden"] is True and tuple(s["result"]) == (16555811, 890536971553)
-    # two shards tile [0, 2^40) in order, each on the stream of the device it names
+    # the two shards' windows (2 slices of 2^39, each cut over both) tile [0, 2^40), each
+    # shard on the stream of the device it names
+    import bench
     sh = s["shards"]
-    assert [x["shard"] for x in sh] == [0, 1] and sh[0]["lo"] == 0 and sh[1]["hi"] == (1 << 40) - 1
-    assert sh[1]["lo"] == sh[0]["hi"] + 1 and sum(x["nonces"] for x in sh) == 1 << 40
+    assert [x["shard"] for x in sh] == [0, 1] and [x["slices"] for x in sh] == [2, 2]
+    assert bench.tiles(sh, 0, (1 << 40) - 1) and sum(x["nonces"] for x in sh) == 1 << 40
     assert all(x["device"] == 0 and x["stream_device"] == [0] for x in sh)
 
 
@@ -133,7 +136,8 @@ def test_bench_torchrun_two_ranks_on_one_gpu(engine):
     s = line["search_2p40"]
     assert s["golden_name"] == "cfg2_bradfitz_2p32" and s["matches_golden"] is True
     assert [x["shard"] for x in s["shards"]] == [0, 1] and s["devices"] == [0, 0]
-    assert s["shards"][1]["lo"] == s["shards"][0]["hi"] + 1 and "device_check" not in line
+    assert s["shards"][1]["windows"][0][0] == s["shards"][0]["windows"][-1][1] + 1
+    assert "device_check" not in line
     # without GPUHASH_SHARE_GPU, a second rank on a 1-GPU box is refused
     import gpuhash
     if gpuhash.device_count() == 1:
