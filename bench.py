@@ -432,6 +432,26 @@ def tiles(rows: list[dict], lo: int, hi: int) -> bool:
         b[0] == a[1] + 1 for a, b in zip(wins, wins[1:]))
 
 
+def pci_id(dev: int) -> str | None:
+    """domain:bus:device of a HIP ordinal (torch's device properties): a physical GPU's
+    identity, whatever ordinal a process's visibility mask gives it."""
+    try:
+        import torch
+        p = torch.cuda.get_device_properties(dev)
+        return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+    except Exception:  # noqa: BLE001 -- evidence only; None says it was unavailable
+        return None
+
+
+def _one_visible_device() -> bool:
+    """True when a visibility variable leaves this process exactly one GPU."""
+    for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(k)
+        if v is not None and len([x for x in v.split(",") if x.strip()]) == 1:
+            return True
+    return False
+
+
 def check_shards(rows: list[dict], devs: list[int]) -> list[str]:
     """Device evidence of a search's shards: shard k ran on devs[k] (the record's ordinal and
     the stream's runtime ordinal agree with it), and -- when the device list has no
@@ -548,7 +568,11 @@ def main_inproc(args, devs: list[int]) -> None:
         barrier()
         sdt = time.perf_counter() - t0
         rows = shard_rows(eng.launches())
+        for r in rows:
+            r["pci"] = pci_id(r["device"])
         problems += check_shards(rows, devs)
+        if len(set(devs)) == len(devs) and len({r["pci"] for r in rows}) != len(rows):
+            problems.append("distinct ordinals requested but two shards share a PCI device")
         if not tiles(rows, lo, hi):
             problems.append("the search's shard windows do not tile its range")
         out["search_2p40"] = search_line(sres, sdt, n, lo, hi, "inproc", devs, rows)
@@ -576,7 +600,11 @@ def main_ranks(args, world: int, rank: int, local: int) -> None:
     if ndev < 1:
         fail("no visible GPU")
     shared = os.environ.get("GPUHASH_SHARE_GPU") == "1"  # rehearsal: ranks share device 0..
-    if local >= ndev and not shared:
+    # a launcher may instead give every rank exactly one visible GPU (HIP/ROCR/CUDA
+    # _VISIBLE_DEVICES): then device 0 is the rank's own GPU, and the PCI check below
+    # proves the ranks' GPUs distinct
+    pinned = ndev == 1 and _one_visible_device()
+    if local >= ndev and not (shared or pinned):
         fail(f"LOCAL_RANK {local} but only {ndev} visible device(s); "
              "set GPUHASH_SHARE_GPU=1 to rehearse several ranks on one GPU")
     local = local % ndev
@@ -640,8 +668,12 @@ def main_ranks(args, world: int, rank: int, local: int) -> None:
         for r in srows:  # one process per GPU: the rank is the shard
             r["shard"] = rank
         search = (sres, sdt, srows)
+    pci = pci_id(local)
+    if search is not None:
+        for r in search[2]:
+            r["pci"] = pci
     gathered = [None] * world
-    dist.all_gather_object(gathered, {"rank": rank, "local_rank": local, "problems": problems,
+    dist.all_gather_object(gathered, {"rank": rank, "local_rank": local, "pci": pci, "problems": problems,
                                       "search_shards": search[2] if search else None})
     if rank == 0:
         value = per_gpu * world * args.steps / dt / 1e9
@@ -650,6 +682,9 @@ def main_ranks(args, world: int, rank: int, local: int) -> None:
         out["result"] = list(res)  # (hash, nonce) argmin over every rank's windows
         out["roofline"] = roof
         problems = [f"rank {g['rank']}: {p}" for g in gathered for p in g["problems"]]
+        out["rank_devices"] = [{"rank": g["rank"], "device": g["local_rank"], "pci": g["pci"]} for g in gathered]
+        if not shared and len({g["pci"] for g in gathered}) != world:
+            problems.append("ranks on distinct GPUs expected but two ranks share a PCI device")
         if search is not None:
             shards = [s for g in gathered for s in (g["search_shards"] or [])]
             devices = [g["local_rank"] for g in gathered]
