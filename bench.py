@@ -481,10 +481,11 @@ def search_line(res, dt: float, n: int, lo: int, hi: int, mode: str, devices, sh
 def search_exit(out: dict, problems: list[str]) -> None:
     """Non-zero exit AFTER the line is printed when the search missed its golden or a shard
     ran somewhere other than its device: the line stays readable, the run counts as failed."""
-    s = out.get("search_2p40")
-    if s is not None and s["matches_golden"] is False:
-        print(f"bench.py: search {s['range']} returned {s['result']}, golden {s['golden']}", file=sys.stderr)
-        sys.exit(3)
+    for key in ("search_2p40", "search_2p40_inproc"):
+        s = out.get(key)
+        if s is not None and s.get("matches_golden") is False:
+            print(f"bench.py: {key} {s['range']} returned {s['result']}, golden {s['golden']}", file=sys.stderr)
+            sys.exit(3)
     if problems:
         print("bench.py: device check failed: " + "; ".join(problems), file=sys.stderr)
         sys.exit(3)
@@ -571,7 +572,8 @@ def main_inproc(args, devs: list[int]) -> None:
         for r in rows:
             r["pci"] = pci_id(r["device"])
         problems += check_shards(rows, devs)
-        if len(set(devs)) == len(devs) and len({r["pci"] for r in rows}) != len(rows):
+        pcis = [r["pci"] for r in rows]
+        if len(set(devs)) == len(devs) and None not in pcis and len(set(pcis)) != len(rows):
             problems.append("distinct ordinals requested but two shards share a PCI device")
         if not tiles(rows, lo, hi):
             problems.append("the search's shard windows do not tile its range")
@@ -672,6 +674,40 @@ def main_ranks(args, world: int, rank: int, local: int) -> None:
     if search is not None:
         for r in search[2]:
             r["pci"] = pci
+    # the north_star's own design -- ONE process, one context over all N GPUs, a host
+    # thread + stream per device, 16-byte host argmin -- on the same node: rank 0 repeats
+    # the search in-process over devices 0..N-1 while the other ranks wait at the barrier
+    # (when every rank has a GPU of its own; a GPUHASH_SHARE_GPU rehearsal repeats ordinal
+    # 0), so a torchrun-launched run measures both modes and exercises the in-process path
+    # on DISTINCT devices.  A host-side failure here is recorded, not fatal: it must not cost
+    # the run its ranks' numbers; a wrong result still fails the run (search_exit)
+    inproc = None
+    inproc_devs = [0] * world if shared else (list(range(world)) if ndev >= world and not pinned else None)
+    if args.search is not None and world > 1 and inproc_devs is not None:
+        barrier()
+        if rank == 0:
+            lo, hi = args.search
+            devs = inproc_devs
+            try:
+                with gpuhash.Engine(devs) as all_eng:
+                    t0 = time.perf_counter()
+                    ires = all_eng.min(MSG, lo, hi)
+                    idt = time.perf_counter() - t0
+                    irows = shard_rows(all_eng.launches())
+                for r in irows:
+                    r["pci"] = pci_id(r["device"])
+                iprob = check_shards(irows, devs)
+                if not tiles(irows, lo, hi):
+                    iprob.append("in-process search: shard windows do not tile the range")
+                ipcis = [r["pci"] for r in irows]
+                if len(set(devs)) == len(devs) and None not in ipcis and len(set(ipcis)) != len(irows):
+                    iprob.append("in-process search: two shards share a PCI device")
+                problems += iprob
+                inproc = search_line(ires, idt, world, lo, hi, "inproc (rank 0, one context over all GPUs)",
+                                     devs, irows)
+            except Exception as e:  # noqa: BLE001 -- see above
+                inproc = {"error": f"{type(e).__name__}: {e}", "devices": devs}
+        barrier()
     gathered = [None] * world
     dist.all_gather_object(gathered, {"rank": rank, "local_rank": local, "pci": pci, "problems": problems,
                                       "search_shards": search[2] if search else None})
@@ -683,7 +719,8 @@ def main_ranks(args, world: int, rank: int, local: int) -> None:
         out["roofline"] = roof
         problems = [f"rank {g['rank']}: {p}" for g in gathered for p in g["problems"]]
         out["rank_devices"] = [{"rank": g["rank"], "device": g["local_rank"], "pci": g["pci"]} for g in gathered]
-        if not shared and len({g["pci"] for g in gathered}) != world:
+        pcis = [g["pci"] for g in gathered]
+        if not shared and None not in pcis and len(set(pcis)) != world:
             problems.append("ranks on distinct GPUs expected but two ranks share a PCI device")
         if search is not None:
             shards = [s for g in gathered for s in (g["search_shards"] or [])]
@@ -694,6 +731,8 @@ def main_ranks(args, world: int, rank: int, local: int) -> None:
                 problems.append("ranks on distinct GPUs but search shards share a device")
             if not tiles(shards, *args.search):
                 problems.append("the ranks' search windows do not tile the range")
+            if inproc is not None:
+                out["search_2p40_inproc"] = inproc
         if problems:
             out["device_check"] = problems
         if world == 1:

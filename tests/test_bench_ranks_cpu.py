@@ -1,0 +1,135 @@
+"""CPU: bench.py's torchrun path (main_ranks) end to end over world-size-2 gloo, with the
+HIP engine replaced by an oracle-backed stand-in and torch.cuda by a two-GPU fake -- the
+code the driver's N > 1 scaling run executes (timed steps, the ranks' search leg with
+its gloo merge, rank 0's in-process repeat over all GPUs, the device/PCI checks, the one
+JSON line) with no GPU.  The stand-in is test infrastructure: it hashes with the C
+oracle on the search range (config 1's [0, 9999], whose golden is committed) and returns
+placeholder results for the 2^32 step windows, which the oracle could not scan."""
+import io
+import json
+import os
+import socket
+import sys
+import types
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, ndev, share, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "bitcoin-miner_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    if share:
+        os.environ["GPUHASH_SHARE_GPU"] = "1"
+    import torch
+    import gpuhash
+    import hash_oracle
+    import bench
+    oracle = hash_oracle.load_c_oracle()
+
+    class FakeEngine:
+        """gpuhash.Engine's surface, oracle-backed on small ranges."""
+
+        def __init__(self, devices=None, lib_path=None):
+            self.devs = list(devices)
+            self.recs = []
+
+        def min(self, msg, lo, hi):
+            cuts = gpuhash.shard_range(len(msg), lo, hi, len(self.devs))  # the real planner
+            self.recs = [{"device": self.devs[i], "J": 4, "C2": 0, "EX": 0, "digits": 10, "c": 1,
+                          "shard": i, "stream_device": self.devs[i], "lo": c[0], "hi": c[1],
+                          "nonces": c[1] - c[0] + 1, "ms": 1e-6 * (c[1] - c[0] + 1), "sclk_mhz": 2400.0}
+                         for i, c in enumerate(cuts) if c is not None]
+            if hi - lo < 1_000_000:
+                return oracle.min(msg, lo, hi)
+            return (lo * 2654435761 % (1 << 64), lo)  # placeholder for the 2^32 step windows
+
+        def launches(self):
+            return list(self.recs)
+
+        @property
+        def ndevices(self):
+            return len(self.devs)
+
+        def close(self):
+            pass
+
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *exc):
+            pass
+
+    gpuhash.Engine = FakeEngine
+    props = lambda d: types.SimpleNamespace(pci_domain_id=0, pci_bus_id=0x10 + 0x10 * d, pci_device_id=0)
+    torch.cuda.device_count = lambda: ndev
+    torch.cuda.set_device = lambda d: None
+    torch.cuda.synchronize = lambda d=None: None
+    torch.cuda.get_device_properties = props
+    args = types.SimpleNamespace(gpus=world, steps=2, warmup=1, no_cpu_baseline=True, cpu_seconds=1.0,
+                                 config="2", inproc=None, search=(0, 9999), no_search=False)
+    out = io.StringIO()
+    sys.stdout = out
+    code = 0
+    try:
+        bench.main_ranks(args, world, rank, rank)
+    except SystemExit as e:
+        code = e.code
+    sys.stdout = sys.__stdout__
+    q.put((rank, code, out.getvalue()))
+
+
+def _run(ndev, share):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, ndev, share, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (c, o)) for r, c, o in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=30)
+    code, text = res[0]
+    line = json.loads([x for x in text.splitlines() if x.startswith("{")][-1])
+    return code, line
+
+
+def test_two_ranks_on_two_gpus_search_leg_and_inproc_repeat():
+    code, line = _run(ndev=2, share=False)
+    assert code in (0, None), line.get("device_check")
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "dp2"
+    s = line["search_2p40"]
+    # each rank searched its cost-balanced window of [0, 9999]; gloo merge = config 1's golden
+    assert s["golden_name"] == "cfg1_bradfitz_9999" and s["matches_golden"] is True
+    assert tuple(s["result"]) == (1419516646206828, 9898)
+    assert [x["shard"] for x in s["shards"]] == [0, 1] and [x["device"] for x in s["shards"]] == [0, 1]
+    assert s["shards"][0]["pci"] != s["shards"][1]["pci"]
+    # rank 0's in-process repeat over devices [0, 1], same golden
+    si = line["search_2p40_inproc"]
+    assert si["matches_golden"] is True and si["devices"] == [0, 1]
+    assert [x["device"] for x in si["shards"]] == [0, 1]
+    assert line["rank_devices"] == [{"rank": 0, "device": 0, "pci": "0000:10:00"},
+                                    {"rank": 1, "device": 1, "pci": "0000:20:00"}]
+    assert "device_check" not in line
+
+
+def test_shared_gpu_rehearsal_repeats_ordinal_zero():
+    code, line = _run(ndev=1, share=True)
+    assert code in (0, None)
+    assert line["search_2p40"]["matches_golden"] is True
+    assert line["search_2p40_inproc"]["devices"] == [0, 0]
+    assert "device_check" not in line

@@ -119,6 +119,7 @@ def test_bench_gpus_above_visible_fails_loudly():
 
 
 def test_bench_torchrun_two_ranks_on_one_gpu(engine):
+    import bench
     port = _free_port()
     launcher = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                 "--master-addr", "127.0.0.1", "--master-port", str(port)]
@@ -138,6 +139,11 @@ def test_bench_torchrun_two_ranks_on_one_gpu(engine):
     assert [x["shard"] for x in s["shards"]] == [0, 1] and s["devices"] == [0, 0]
     assert s["shards"][1]["windows"][0][0] == s["shards"][0]["windows"][-1][1] + 1
     assert "device_check" not in line
+    # rank 0 repeats the search in-process over one context of N entries (here ordinal 0
+    # twice; on an 8-GPU node devices 0..7), checked against the same golden
+    si = line["search_2p40_inproc"]
+    assert si["matches_golden"] is True and si["devices"] == [0, 0]
+    assert [x["shard"] for x in si["shards"]] == [0, 1] and bench.tiles(si["shards"], 0, (1 << 32) - 1)
     # without GPUHASH_SHARE_GPU, a second rank on a 1-GPU box is refused
     import gpuhash
     if gpuhash.device_count() == 1:
