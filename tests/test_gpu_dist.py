@@ -144,9 +144,13 @@ def test_bench_torchrun_two_ranks_on_one_gpu(engine):
     si = line["search_2p40_inproc"]
     assert si["matches_golden"] is True and si["devices"] == [0, 0]
     assert [x["shard"] for x in si["shards"]] == [0, 1] and bench.tiles(si["shards"], 0, (1 << 32) - 1)
-    # without GPUHASH_SHARE_GPU, a second rank on a 1-GPU box is refused
+    # without GPUHASH_SHARE_GPU, two ranks on a 1-GPU box must fail loudly: refused at
+    # start, or -- when a *_VISIBLE_DEVICES variable leaves each process one GPU, which
+    # bench.py accepts as one GPU per rank -- by the PCI check once both ranks report the
+    # same physical GPU (exit 3 after the line)
     import gpuhash
     if gpuhash.device_count() == 1:
-        r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"],
-                   launcher=launcher[:-1] + [str(_free_port())])
-        assert r.returncode != 0 and "LOCAL_RANK 1" in r.stderr
+        r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu-baseline",
+                    "--search", "0:4294967295"], launcher=launcher[:-1] + [str(_free_port())])
+        assert r.returncode != 0
+        assert "LOCAL_RANK 1" in r.stderr or "share a PCI device" in r.stderr, r.stderr[-1500:]
