@@ -170,3 +170,30 @@ def test_go_binding_matches_the_header():
         elif ident not in protos:  # a type, e.g. gpuhash_ctx
             assert re.search(r"typedef\s+struct\s+" + ident + r"\b", hdr), ident
     assert {"gpuhash_open", "gpuhash_min", "gpuhash_close"} <= used
+
+
+def test_ctypes_structs_match_the_header(tmp_path):
+    """gpuhash.Stats / gpuhash.LaunchRecord lay out exactly like the header's structs (a C
+    program compiled against include/gpuhash.h prints sizeof/offsetof): a field added to
+    the header without the mirror -- or in another order -- would shift every later field
+    the bench and the tests read."""
+    import ctypes
+    import subprocess
+    import gpuhash
+    fields = {"gpuhash_stats": [f for f, _ in gpuhash.Stats._fields_],
+              "gpuhash_launch_record": [f for f, _ in gpuhash.LaunchRecord._fields_]}
+    src = ["#include <stdio.h>", "#include <stddef.h>", '#include "gpuhash.h"', "int main(void) {"]
+    for st, fs in fields.items():
+        src.append(f'  printf("{st} %zu\\n", sizeof({st}));')
+        for f in fs:
+            src.append(f'  printf("{st}.{f} %zu\\n", offsetof({st}, {f}));')
+    src += ["  return 0;", "}"]
+    c = tmp_path / "layout.c"
+    c.write_text("\n".join(src) + "\n")
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(c), "-o", str(exe)])
+    got = dict(line.rsplit(" ", 1) for line in subprocess.check_output([str(exe)], text=True).splitlines())
+    for st, cls in (("gpuhash_stats", gpuhash.Stats), ("gpuhash_launch_record", gpuhash.LaunchRecord)):
+        assert int(got[st]) == ctypes.sizeof(cls), st
+        for f, _ in cls._fields_:
+            assert int(got[f"{st}.{f}"]) == getattr(cls, f).offset, (st, f)
