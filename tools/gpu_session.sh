@@ -2,7 +2,7 @@
 # tools/gpu_session.sh STEP... -- runs GPU steps on the gpurun box, each under its own
 # time limit, logging to gpurun_out/.  A plain failure (exit 1, e.g. a failing test)
 # lets the next step run; a fault, abort, segfault, time limit or kill stops the session.
-# Steps: fma | cumask | family | inproc8c4 | valu | go | test | soak | smoke | bench | bench3 | bench4 | prof4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | pmc3 | pmc4 | sweep | variants | partial | regret | sys5
+# Steps: inproc8s | dist8s | fma | cumask | family | inproc8c4 | valu | go | test | soak | smoke | bench | bench3 | bench4 | prof4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | pmc3 | pmc4 | sweep | variants | partial | regret | sys5
 set -u
 cd "$(dirname "$0")/.."
 OUT=gpurun_out
@@ -38,6 +38,8 @@ for step in "$@"; do
         systest) run pytest_sys 600 python -u -m pytest tests/test_gpu_system.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 300 python -u bench.py --steps 10 --warmup 2 ;;
+        inproc8s) run inproc8s 300 python -u bench.py --inproc 0,0,0,0,0,0,0,0 --steps 2 --warmup 1 --no-cpu-baseline ;;
+        dist8s) run dist8s 400 env GPUHASH_SHARE_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29549 bench.py --gpus 8 --steps 1 --warmup 1 ;;
         inproc40) run inproc40 300 python -u bench.py --inproc 0,0 --steps 2 --warmup 1 --no-cpu-baseline ;;
         nccl1) run nccl1 300 env GPUHASH_FORCE_DIST=1 GPUHASH_DIST_BACKEND=nccl python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29541 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
         dist2) run dist2 300 env GPUHASH_SHARE_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 ;;
