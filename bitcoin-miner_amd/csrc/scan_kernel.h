@@ -86,8 +86,24 @@ __device__ __forceinline__ uint32_t bs1(uint32_t x) { return xor3(rotr(x, 17), r
 
 // Wave-uniform primitives: plain C so the compiler keeps them on SALU.
 __device__ __forceinline__ uint32_t urotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+#ifdef GPUHASH_SALU_SIGMA
+// Tuning hook (tools/build_fold_variants.sh, off in the product build): LLVM turns the
+// uniform sigma0(W_J) into v_alignbit with SGPR sources (VALU); this pins it on SALU as
+// the low word of the 64-bit shift of the pair {x, x}.  Measured 2.6% SLOWER on config
+// 2 (profiles/r04_fold_variants.jsonl).
+template <int N>
+__device__ __forceinline__ uint32_t srotr(uint32_t x) {
+    const unsigned long long p = ((unsigned long long)x << 32) | x;
+    unsigned long long r;
+    asm("s_lshr_b64 %0, %1, %2" : "=s"(r) : "s"(p), "i"(N));
+    return (uint32_t)r;
+}
+__device__ __forceinline__ uint32_t us0(uint32_t x) { return srotr<7>(x) ^ srotr<18>(x) ^ (x >> 3); }
+__device__ __forceinline__ uint32_t us1(uint32_t x) { return srotr<17>(x) ^ srotr<19>(x) ^ (x >> 10); }
+#else
 __device__ __forceinline__ uint32_t us0(uint32_t x) { return urotr(x, 7) ^ urotr(x, 18) ^ (x >> 3); }
 __device__ __forceinline__ uint32_t us1(uint32_t x) { return urotr(x, 17) ^ urotr(x, 19) ^ (x >> 10); }
+#endif
 
 __device__ __forceinline__ uint32_t ascii4(uint32_t x) {
     uint32_t x1 = x / 10u, x2 = x1 / 10u, x3 = x2 / 10u;
@@ -125,6 +141,22 @@ __device__ __forceinline__ void round_kw(State& s, uint32_t kw) {
     s.d = s.c; s.c = s.b; s.b = s.a; s.a = t1 + t2;
 }
 
+// A round whose K+W is wave-uniform (an SGPR) and whose h is per-lane.  A 2-input VALU
+// add with a scalar operand issues at the slow rate; left to itself LLVM
+// reads `kw` in the 2-input h + kw.  Here it goes into the 3-input add, slow class
+// anyway, so the round's 2-input adds read VGPRs only.  The K+W-table layout (config 3)
+// runs +1.8% with it; the plain, extra-block and lane-table rounds with a uniform K+W run
+// 0.3-3.8% SLOWER with it (tuning hooks GPUHASH_FOLD_{PLAIN,EX,LT}, off in the product
+// build; profiles/r04_fold_variants.jsonl), so only ut_hash's table rounds use it.
+__device__ __forceinline__ void round_ukw(State& s, uint32_t kw) {
+    uint32_t x;
+    asm("v_add3_u32 %0, %1, %2, %3" : "=v"(x) : "v"(s.h), "s"(kw), "v"(ch(s.e, s.f, s.g)));
+    uint32_t t1 = x + bS1(s.e);
+    uint32_t t2 = bS0(s.a) + maj(s.a, s.b, s.c);
+    s.h = s.g; s.g = s.f; s.f = s.e; s.e = s.d + t1;
+    s.d = s.c; s.c = s.b; s.b = s.a; s.a = t1 + t2;
+}
+
 // Message expansion of a block whose words are all per-lane or uniform (no W_J):
 // used for block B-1 of C2 layouts, once per work item.
 __device__ __forceinline__ void expand_full(uint32_t (&w)[64]) {
@@ -148,7 +180,8 @@ struct WaveBest {
 // table, the per-lane input is the state s after block B-1 (= cv), so a nonce costs 64
 // rounds and no schedule work.  Round 0 reuses the per-row part `inv0` (everything but
 // kw[0]); round 63 skips e and folds CV0.
-template <class KW>
+// Rounds t in [SK0, SK1) have a wave-uniform kw(t) (scalar loads) and a per-lane h.
+template <int SK0, int SK1, class KW>
 __device__ __forceinline__ void ut_hash(const dev::State& s, const uint32_t (&cv)[8], uint32_t inv0,
                                         uint32_t t20, KW&& kw, uint32_t& H0, uint32_t& H1) {
     using namespace dev;
@@ -158,7 +191,8 @@ __device__ __forceinline__ void ut_hash(const dev::State& s, const uint32_t (&cv
     x.d = x.c; x.c = x.b; x.b = x.a; x.a = (inv0 + t20) + k0;
     sfor<1, 63>([&](auto tc) {
         constexpr int t = decltype(tc)::value;
-        round_kw(x, kw(t));
+        if constexpr (t >= SK0 && t < SK1) round_ukw(x, kw(t));
+        else round_kw(x, kw(t));
     });
     const uint32_t t1 = x.h + kw(63) + cv[0] + ch(x.e, x.f, x.g) + bS1(x.e);
     H0 = t1 + bS0(x.a) + maj(x.a, x.b, x.c);
@@ -312,7 +346,7 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
             for (uint32_t j = 0; j < (wave_idle ? 0u : nb); j++) {
                 const uint4* kr = sh_kw[j];
                 uint32_t H0, H1;
-                ut_hash(s, cv, inv0, t20, [&](int t) {
+                ut_hash<0, 0>(s, cv, inv0, t20, [&](int t) {   // kw from LDS: per-lane
                     const uint4 v = kr[t >> 2];
                     return (t & 3) == 0 ? v.x : (t & 3) == 1 ? v.y : (t & 3) == 2 ? v.z : v.w;
                 }, H0, H1);
@@ -328,7 +362,7 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
         uint32_t H0, H1;
         if constexpr (UT) {
             const uint32_t* __restrict__ kw = ktab + D.tab_off + 64u * r;
-            ut_hash(s, cv, inv0, t20, [&](int t) { return kw[t]; }, H0, H1);
+            ut_hash<1, 63>(s, cv, inv0, t20, [&](int t) { return kw[t]; }, H0, H1);
         } else {
             const uint32_t WJ = D.U[J] | ((ascii4(r) & D.qmask) << D.loop_shift);
             uint32_t w[64];
@@ -367,7 +401,14 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
                 if constexpr (t >= 20) asm volatile("s_xor_b32 %0, %0, %1" : "+s"(salu_dummy) : "i"(K[t]));
 #endif
                 if constexpr (t < 16) {
+#ifdef GPUHASH_FOLD_PLAIN
+                    // tuning hook (round_ukw above; 3% slower on config 2): h = e_{t-3} is
+                    // per-lane from round J+2 on (C2 = 0: rounds before J-2 are the host's)
+                    if constexpr (C2 == 0 && t >= J + 2) round_ukw(x, K[t] + w[t]);
+                    else round_kw(x, K[t] + w[t]);
+#else
                     round_kw(x, K[t] + w[t]);   // uniform word: K+W folds
+#endif
                 } else {
                     sched(tc);
                     round_kw(x, w[t] + K[t]);
@@ -386,7 +427,11 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
                 const uint32_t y0 = y.a, y1 = y.b;
                 sfor<0, 63>([&](auto tc) {
                     constexpr int t = decltype(tc)::value;
+#ifdef GPUHASH_FOLD_EX
+                    round_ukw(y, D.KWX[t]);   // tuning hook (round_ukw above): no gain
+#else
                     round_kw(y, D.KWX[t]);
+#endif
                 });
                 uint32_t t1 = y.h + D.KWX[63] + ch(y.e, y.f, y.g) + bS1(y.e);
                 H0 = y0 + t1 + bS0(y.a) + maj(y.a, y.b, y.c);
@@ -437,7 +482,12 @@ __device__ __forceinline__ void scan_row_lt(const LaunchDesc& D, uint32_t row, u
         for (int i = 0; i < 8; i++) cv[i] = P[i];
         const State s{cv[0], cv[1], cv[2], cv[3], cv[4], cv[5], cv[6], cv[7]};
         uint32_t H0, H1;
-        ut_hash(s, cv, P[8], P[9], [&](int t) { return kw[t]; }, H0, H1);
+        // kw[2..15] = K + the message's constant words (uniform); h is per-lane from round 4
+#ifdef GPUHASH_FOLD_LT  // tuning hook (round_ukw above): 3.8% slower
+        ut_hash<4, 16>(s, cv, P[8], P[9], [&](int t) { return kw[t]; }, H0, H1);
+#else
+        ut_hash<0, 0>(s, cv, P[8], P[9], [&](int t) { return kw[t]; }, H0, H1);
+#endif
 #ifdef GPUHASH_TIE_TEST_BITS
         H0 >>= (32 - GPUHASH_TIE_TEST_BITS);
         H1 = 0;

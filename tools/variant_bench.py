@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 VDIR = os.path.join(ROOT, "tools", "variants")
 
 CHILD = r'''
-import json, sys, time
+import json, os, sys, time
 sys.path.insert(0, sys.argv[2])
 import gpuhash
 M120 = (b"The quick brown fox jumps over the lazy dog. " * 3)[:120]
@@ -29,13 +29,21 @@ with gpuhash.Engine([0], lib_path=sys.argv[1]) as e:
              ("u2p", b"u" * 60, 10**9, (1 << 32) - 1),  # C2=2, 430 lane values: wave 3 of row 2 idle
              ("lt61", b"t" * 61, 10**9, 10**9 + (1 << 31)),        # C2=3 lane table, 2 digits in B-1
              ("lt58", b"t" * 58, 10**11, 10**11 + (1 << 32))]     # C2=3 lane table, 5 digits in B-1
+    only = os.environ.get("VCASES")
+    if only:
+        cases = [next(c for c in cases if c[0] == n) for n in only.split(",")]
     for name, msg, lo, hi in cases:
         e.min(msg, lo, hi)
-        best, res = 1e9, None
+        best, res, sclk = 1e9, None, None
         for _ in range(4):
             t = time.perf_counter(); res = e.min(msg, lo, hi); dt = time.perf_counter() - t
-            best = min(best, dt)
-        out[name] = {"GHs": (hi - lo + 1) / best / 1e9, "res": list(res)}
+            if dt < best:
+                best = dt
+                # in-kernel shader clock of the launch with the most nonces (workgroup 0's
+                # s_memtime / s_memrealtime over the persistent launch)
+                top = max(e.launches(), key=lambda l: l["nonces"])
+                sclk = top["sclk_mhz"]
+        out[name] = {"GHs": (hi - lo + 1) / best / 1e9, "res": list(res), "sclk": sclk}
     print(json.dumps(out))
 '''
 
@@ -54,6 +62,7 @@ for rnd in range(rounds):
         d = json.loads(r.stdout.strip().splitlines()[-1])
         results[n].append(d)
         print(json.dumps({"variant": n, "round": rnd, **{k: round(v["GHs"], 3) for k, v in d.items()}}), flush=True)
+        print(json.dumps({"variant": n, "round": rnd, "sclk_mhz": {k: v["sclk"] and round(v["sclk"]) for k, v in d.items()}}), flush=True)
 ref = None
 for n, ds in results.items():
     if not ds:
