@@ -10,7 +10,15 @@
 set -eu
 cd "$(dirname "$0")/.."
 HIPCC=/opt/rocm/bin/hipcc
-INC="-Iinclude -Ibitcoin-miner_amd/csrc"
+# the ahead<L> variants need the GPUHASH_SCHED_AHEAD hook (tools/sched_ahead.patch: schedule
+# word t+L written before round t), applied to a temporary copy of the sources so the
+# product sources, and so the product build id, stay untouched
+TMP=$(mktemp -d)
+trap 'rm -rf "$TMP"' EXIT
+mkdir -p "$TMP/bitcoin-miner_amd"
+cp -r bitcoin-miner_amd/csrc "$TMP/bitcoin-miner_amd/csrc"
+patch -s -p1 -d "$TMP" < tools/sched_ahead.patch
+INC="-Iinclude -I$TMP/bitcoin-miner_amd/csrc"
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC $INC -Wno-unused-result -Wno-unused-value -DGPUHASH_WAVES_PER_EU=8"
 B=bitcoin-miner_amd/build
 mkdir -p tools/variants/product
@@ -23,13 +31,17 @@ declare -A OPT=(
   [s_nohrp]="-mllvm -amdgpu-disable-unclustered-high-rp-reschedule"
   [s_noclus]="-mllvm -amdgpu-disable-clustered-low-occupancy-reschedule"
   [s_memclause]="-mllvm -amdgpu-sched-strategy=max-memory-clause"
+  [ahead1]="-DGPUHASH_SCHED_AHEAD=1"
+  [ahead2]="-DGPUHASH_SCHED_AHEAD=2"
+  [ahead3]="-DGPUHASH_SCHED_AHEAD=3"
+  [ahead5]="-DGPUHASH_SCHED_AHEAD=5"
 )
 names=${SCHED_VARIANTS:-${!OPT[@]}}
 for name in $names; do
   (
     out=tools/variants/$name
     mkdir -p "$out"
-    if $HIPCC $F ${OPT[$name]} -c bitcoin-miner_amd/csrc/kernels_plain.hip -o "$out/kernels_plain.o" 2> "$out/build.log"; then
+    if $HIPCC $F ${OPT[$name]} -c $TMP/bitcoin-miner_amd/csrc/kernels_plain.hip -o "$out/kernels_plain.o" 2> "$out/build.log"; then
       $HIPCC --offload-arch=gfx950 -shared -fPIC -o "$out/libgpuhash.so" $B/kernels.o "$out/kernels_plain.o" \
           $B/kernels_ut.o $B/kernels_misc.o $B/gpuhash.o $B/plan_hip.o -lpthread
       [ -n "${KEEP_OBJ:-}" ] && mkdir -p "$KEEP_OBJ/$name" && cp "$out/kernels_plain.o" "$KEEP_OBJ/$name/"
