@@ -336,7 +336,7 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
         const Launch* big = nullptr;
         for (size_t k : groups[g].idx) {
             const Launch& l = plan[k];
-            uint64_t n = l.hi - l.lo + 1;
+            uint64_t n = (l.hi - l.lo) / l.stride + 1;
             nonces += n;
             if (!big || n > biggest) { big = &l; biggest = n; }
         }
@@ -435,7 +435,11 @@ int gpuhash_shard_range(size_t msg_len, uint64_t lower, uint64_t upper, int nsha
 }
 
 int gpuhash_set_layout_policy(gpuhash_ctx* ctx, int policy) {
-    if (!ctx || policy < GPUHASH_LAYOUT_AUTO || policy > GPUHASH_LAYOUT_LANETABLE) return GPUHASH_EINVAL;
+    const int base = policy & 15, flags = policy & ~15;
+    if (!ctx || base < GPUHASH_LAYOUT_AUTO || base > GPUHASH_LAYOUT_LANETABLE ||
+        (flags & ~(GPUHASH_LAYOUT_TAIL_ALWAYS | GPUHASH_LAYOUT_TAIL_NEVER)) ||
+        flags == (GPUHASH_LAYOUT_TAIL_ALWAYS | GPUHASH_LAYOUT_TAIL_NEVER))
+        return GPUHASH_EINVAL;
     std::lock_guard<std::mutex> lock(ctx->mu);
     ctx->policy = policy;
     return GPUHASH_OK;

@@ -24,6 +24,7 @@ struct gpuhash_plan_info {
     int J, C2, EX, d, q, s;
     uint64_t lo, hi, base;
     uint32_t nblocks, R, rchunk, nrchunks, p_first, p_last, r_first, r_last;
+    uint32_t stride, tail;  // tail-digit launches: nonces = tail (mod stride) in [lo, hi]
 };
 
 int gpuhash_plan_count(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper,
@@ -43,7 +44,8 @@ int gpuhash_plan_get(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t 
     const Launch& l = v[(size_t)idx];
     const LaunchDesc& D = l.desc;
     *out = gpuhash_plan_info{l.J, l.C2, l.EX, l.d, l.q, l.s, l.lo, l.hi, D.base, l.nblocks,
-                             D.R, D.rchunk, D.nrchunks, D.p_first, D.p_last, D.r_first, D.r_last};
+                             D.R, D.rchunk, D.nrchunks, D.p_first, D.p_last, D.r_first, D.r_last,
+                             D.stride, D.tail};
     return 0;
 }
 
@@ -57,7 +59,8 @@ int gpuhash_plan_all(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t 
         const Launch& l = v[(size_t)i];
         const LaunchDesc& D = l.desc;
         out[i] = gpuhash_plan_info{l.J, l.C2, l.EX, l.d, l.q, l.s, l.lo, l.hi, D.base, l.nblocks,
-                                   D.R, D.rchunk, D.nrchunks, D.p_first, D.p_last, D.r_first, D.r_last};
+                                   D.R, D.rchunk, D.nrchunks, D.p_first, D.p_last, D.r_first, D.r_last,
+                                   D.stride, D.tail};
     }
     return (int)v.size();
 }
@@ -102,7 +105,10 @@ int hostcheck_desc_hash(const uint8_t* msg, uint64_t len, uint64_t lower, uint64
         *out = ((uint64_t)(P[0] + s1[0]) << 32) | (uint32_t)(P[1] + s1[1]);
         return 0;
     }
-    const uint64_t off = nonce - D.base;
+    // tail-digit launch: the kernel iterates k = nonce / stride; the tail digit is a
+    // constant byte of D.U
+    if (nonce % D.stride != D.tail) return -2;
+    const uint64_t off = nonce / D.stride - D.base;
     const uint32_t p = (uint32_t)(off / D.R), r = (uint32_t)(off % D.R);
     const uint32_t alo = ascii4(p % 10000u), ahi = ascii4((p / 10000u) % 10000u);
     uint32_t W[64], st[8], cv[8];

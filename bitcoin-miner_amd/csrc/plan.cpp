@@ -111,6 +111,8 @@ namespace {
 
 struct GroupLayout {
     int d, J, q, s, C2, EX;
+    int u;       // 1: a tail-digit layout -- d counts the digits of k = nonce / 10, the
+                 //    last digit follows them as a constant message byte (plan.h)
     int q1;      // C2 = 2: digits of W_1 (q = 4 + q1)
     uint64_t B;  // index of the block holding the last digit
 };
@@ -130,6 +132,7 @@ GroupLayout layout_for(uint64_t m, int d, uint64_t span = 0, int policy = kLayou
     int before = d - g.q;
     g.s = std::min(std::min(kMaxLane, before), kMaxLaunchDigits - g.q);
     if (g.s < 0) g.s = 0;
+    g.u = 0;
     uint64_t blkB = 64 * g.B;
     // digit bytes of block B that precede word J
     uint64_t nbB = (f_abs >= wstart) ? 0 : wstart - std::max(f_abs, blkB);
@@ -183,6 +186,26 @@ GroupLayout layout_for(uint64_t m, int d, uint64_t span = 0, int policy = kLayou
     return g;
 }
 
+// Tail-digit layout of plain digit group d (plan.h): when its last digit-bearing word W_J
+// holds one digit and W_{J-1} four, the nonces = t (mod 10) of the group are searched as
+// k = nonce / 10 with t a constant byte after k's digits, so the loop word is W_{J-1}
+// (R = 10^4) instead of W_J (R = 10: a row's setup -- lane words, two rounds, the
+// schedule terms that do not read the loop word, ~255 VALU per lane -- amortised over 10
+// nonces costs ~2.6%, tools/q1_probe.py).  The per-nonce work is the J-1 kernel's, one
+// round more.  Returns false when the group does not qualify.
+bool tail_layout(uint64_t m, int d, const GroupLayout& g, GroupLayout& out) {
+    if (g.C2 || g.q != 1 || g.J < 2 || d < 6) return false;
+    GroupLayout k = layout_for(m, d - 1);
+    // the same final block, k's last digit ending W_{J-1}, four loop digits, no spill into
+    // block B-1; the extra-block flag follows the real length (k's last byte is one
+    // before the tail's, and 4 | tail byte, so both read >= 55 alike)
+    if (k.C2 || k.B != g.B || k.J != g.J - 1 || k.q != 4 || k.EX != g.EX) return false;
+    if (k.EX && k.J < 13) return false;
+    k.u = 1;
+    out = k;
+    return true;
+}
+
 inline uint32_t low_bytes_mask(int nbytes) {
     if (nbytes <= 0) return 0u;
     if (nbytes >= 4) return 0xFFFFFFFFu;
@@ -208,10 +231,13 @@ Prefix make_prefix(const uint8_t* msg, uint64_t m) {
     return p;
 }
 
+// [lo, hi]: the launch's nonces, or for a tail-digit layout (g.u = 1) its k = nonce / 10
+// values, whose nonces end in the digit `tail`.
 void build_launch(const uint8_t* msg, uint64_t m, const Prefix& pre, const GroupLayout& g, uint64_t H,
-                  uint64_t lo, uint64_t hi, uint32_t rchunk_max, Launch& out, bool host_ptab) {
+                  uint64_t lo, uint64_t hi, uint32_t rchunk_max, Launch& out, bool host_ptab,
+                  uint32_t tail = 0) {
     const int d = g.d, q = g.q, s = g.s, h = d - s - q;
-    const uint64_t L = m + 1 + (uint64_t)d;
+    const uint64_t L = m + 1 + (uint64_t)d + (uint64_t)g.u;
     const uint64_t nblk = g.B + 1 + (uint64_t)g.EX;
     const uint64_t first_var = g.C2 ? g.B - 1 : g.B;
     // pre.blocks <= first_var: the first digit is at byte m+1, and block B-1 of a C2
@@ -224,6 +250,7 @@ void build_launch(const uint8_t* msg, uint64_t m, const Prefix& pre, const Group
     uint64_t v = H;
     for (int i = h - 1; i >= 0; i--) { buf[m + 1 + (uint64_t)i - base] = (uint8_t)('0' + v % 10u); v /= 10u; }
     // lane + loop digit bytes stay 0: the kernel ORs ASCII into them
+    if (g.u) buf[L - 1 - base] = (uint8_t)('0' + tail);
     buf[L - base] = 0x80;
     uint64_t bits = L * 8u;
     for (int i = 0; i < 8; i++) buf[(nblk - p0) * 64 - 1 - (uint64_t)i] = (uint8_t)(bits >> (8 * i));
@@ -269,7 +296,7 @@ void build_launch(const uint8_t* msg, uint64_t m, const Prefix& pre, const Group
     D.mask_hi = low_bytes_mask(s - 4);
     D.qmask = low_bytes_mask(g.C2 >= 2 ? g.q1 : q);
     D.R1 = g.C2 >= 2 ? (uint32_t)pow10u(g.q1) : 1u;
-    const int e = (int)((L - 1) % 64);
+    const int e = (int)((L - 1 - (uint64_t)g.u) % 64);  // the last (loop) digit's byte
     D.loop_shift = (uint32_t)(3 - e % 4) * 8u;
     if (g.C2 == 3) {
         // lane table: lanes = the q digits of W_0/W_1 (x in [x_a, x_b]), loop = the s digits
@@ -288,6 +315,9 @@ void build_launch(const uint8_t* msg, uint64_t m, const Prefix& pre, const Group
         D.r_last = NP - 1u;
         D.base = H * U + p_a * RQ;
         D.lt_p0 = (uint32_t)p_a;
+        D.stride = 1u;
+        D.tail = 0u;
+        out.stride = 1u;
         out.nptab = 16u * NP;
         // p-table: block B-1 with the s loop digits of p (its last s bytes), compressed
         // from CV1, then round 0 of block B up to its K+W term.  The library builds it on
@@ -331,11 +361,14 @@ void build_launch(const uint8_t* msg, uint64_t m, const Prefix& pre, const Group
     D.p_last = (uint32_t)((hi / R) % P);
     D.r_last = (uint32_t)(hi % R);
     D.base = H * R * P;
+    D.stride = g.u ? 10u : 1u;
+    D.tail = tail;
 
     out.J = g.J; out.C2 = g.C2; out.EX = g.EX;
-    out.d = d; out.q = q; out.s = s;
+    out.d = d + g.u; out.q = q; out.s = s;
     out.c = ((m + 1) / 64 != (L - 1) / 64) ? 2 : 1;
-    out.lo = lo; out.hi = hi;
+    out.stride = D.stride;
+    out.lo = lo * D.stride + tail; out.hi = hi * D.stride + tail;
     uint32_t npb = (D.p_last - D.p_first) / (uint32_t)kBlock + 1u;
     out.nblocks = npb * D.nrchunks;
 }
@@ -352,7 +385,30 @@ void plan_range(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper
         a = std::max(a, lower);
         b = std::min(b, upper);
         if (a > b) continue;
-        GroupLayout g = layout_for(len, d, b - a == UINT64_MAX ? 0 : b - a + 1, policy);
+        const uint64_t span = b - a == UINT64_MAX ? 0 : b - a + 1;
+        GroupLayout g = layout_for(len, d, span, policy & kLayoutMask);
+        GroupLayout gt;
+        const bool tail = !(policy & kLayoutTailNever) &&
+                          ((policy & kLayoutTailAlways) || span == 0 || span >= kTailMinSpan) &&
+                          tail_layout(len, d, g, gt);
+        if (tail) {
+            // ten launch sets, one per last digit t: k = nonce / 10 over the nonces = t (mod
+            // 10) of [a, b] (a >= 10^(d-1) >= 10, so every k has d-1 digits)
+            for (uint32_t t = 0; t < 10; t++) {
+                if (b < t) continue;
+                const uint64_t ka = a <= t ? 0 : (a - t + 9) / 10, kb = (b - t) / 10;
+                if (ka > kb) continue;
+                const uint64_t Uk = pow10u(gt.s + gt.q);
+                for (uint64_t H = ka / Uk;; H++) {
+                    Launch l;
+                    build_launch(msg, len, pre, gt, H, std::max(ka, H * Uk),
+                                 H == kb / Uk ? kb : H * Uk + (Uk - 1), rchunk_max, l, host_ptab, t);
+                    out.push_back(std::move(l));
+                    if (H == kb / Uk) break;
+                }
+            }
+            continue;
+        }
         const uint64_t U = pow10u(g.s + g.q);
         const uint64_t Hf = a / U, Hl = b / U;
         for (uint64_t H = Hf;; H++) {

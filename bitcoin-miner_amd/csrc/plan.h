@@ -25,6 +25,11 @@
 //     uniform     : prefix bytes, H's digits, 0x80, zero pad, bit length -> host
 //                    precomputes the midstate, the uniform words and the rounds that
 //                    only read uniform words
+//   tail digit    (plain layouts whose last digit-bearing word holds ONE digit: a loop of
+//                  only 10 values per row, whose per-row setup then costs ~2.6%) the last
+//                  digit t is fixed per launch: ten launches, one per t, each searching the
+//                  nonces = t (mod 10) as k = nonce / 10 with t a constant message byte, so
+//                  the loop word is the previous, 4-digit word (R = 10^4)
 //   work item     (a group of 256 consecutive lane values p) × (a chunk of r values)
 //                 = one workgroup of the kernel
 //
@@ -74,6 +79,10 @@ struct LaunchDesc {
     uint32_t RQ;       // C2 = 3: 10^q, lane values per loop value
     uint64_t base;     // nonce = base + p·R + r  (C2 = 3: base + r·RQ + p, p = lane value)
     uint32_t lt_p0;    // C2 = 3: block B-1 value of loop value 0 (p-table entry k: lt_p0 + k)
+    // tail-digit launches (below): the kernel's k = base + p·R + r is the nonce without its
+    // last digit, nonce = k·stride + tail; plain launches: stride 1, tail 0
+    uint32_t stride;
+    uint32_t tail;
     uint32_t pad2_;
 };
 
@@ -83,7 +92,8 @@ struct Launch {
     int EX;         // extra constant padding block
     int d, q, s;    // digits, loop digits, lane digits
     int c;          // 64-byte blocks that hold nonce digits (the SURVEY 8(d) "c")
-    uint64_t lo, hi;      // inclusive nonce range covered
+    uint64_t lo, hi;      // first and last nonce covered (every stride-th nonce from lo)
+    uint32_t stride = 1;  // 10 for a tail-digit launch: the nonces = tail (mod 10) in [lo, hi]
     uint32_t nblocks;     // grid size (workgroups of 256)
     LaunchDesc desc;
     uint32_t nptab = 0;          // C2 = 3: p-table words (16 per loop value, LaunchDesc::tab_off)
@@ -102,6 +112,12 @@ static constexpr int kMaxLaunchDigitsU2 = 12;
 // Choice between the J = 1 straddling layouts (plan.cpp layout_for); the rule is stated
 // once, in include/gpuhash.h above GPUHASH_LAYOUT_AUTO.
 enum LayoutPolicy { kLayoutAuto = 0, kLayoutUniform = 1, kLayoutClassic = 2, kLayoutLaneTable = 3 };
+// policy flags for the tail-digit layouts (include/gpuhash.h): taken for digit groups the
+// search spans kTailMinSpan nonces of, or always / never with the flags
+static constexpr int kLayoutMask = 15;
+static constexpr int kLayoutTailAlways = GPUHASH_LAYOUT_TAIL_ALWAYS;
+static constexpr int kLayoutTailNever = GPUHASH_LAYOUT_TAIL_NEVER;
+static constexpr uint64_t kTailMinSpan = GPUHASH_TAIL_MIN_SPAN;
 // C2 = 3: at most this many loop values (p-table entries) per launch, and AUTO / LANETABLE
 // take the layout only for searches touching at most kMaxLtTable block B-1 values (4 MB)
 static constexpr uint32_t kMaxLtLoop = 1024;

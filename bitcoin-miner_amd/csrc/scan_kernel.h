@@ -295,7 +295,8 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
 #endif
         if constexpr (MODE == 1) {
             if (lane_ok && r >= rlo && r <= rhi) {
-                unsigned long long n = D.base + (unsigned long long)p * D.R + r;
+                // k = D.base + p·R + r; nonce = k·stride + tail (tail-digit launches, plan.h)
+                unsigned long long n = (D.base + (unsigned long long)p * D.R + r) * D.stride + D.tail;
                 dump[n - dump_lo] = ((unsigned long long)H0 << 32) | H1;
             }
         } else {
@@ -310,7 +311,7 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
                     const uint32_t h1 = __builtin_amdgcn_readlane(H1, l);
                     const uint32_t pl = __builtin_amdgcn_readlane(p, l);
                     const unsigned long long hh = ((unsigned long long)h0 << 32) | h1;
-                    const unsigned long long nn = D.base + (unsigned long long)pl * D.R + r;
+                    const unsigned long long nn = (D.base + (unsigned long long)pl * D.R + r) * D.stride + D.tail;
                     if (hh < wb.h || (hh == wb.h && nn < wb.n)) {
                         wb.h = hh;
                         wb.n = nn;

@@ -36,6 +36,9 @@ GPUHASH_ETOOLONG = -4
 GPUHASH_ENOMEM = -5
 GPUHASH_MAX_MSG = 1 << 20
 LAYOUT_AUTO, LAYOUT_UNIFORM, LAYOUT_CLASSIC, LAYOUT_LANETABLE = 0, 1, 2, 3
+# OR-able flags: tail-digit launches always / never (include/gpuhash.h)
+LAYOUT_TAIL_ALWAYS, LAYOUT_TAIL_NEVER = 16, 32
+TAIL_MIN_SPAN = 1 << 33
 
 # Every symbol include/gpuhash.h declares (tests check the .so exports all of them).
 EXPORTED = [
@@ -200,8 +203,8 @@ class Engine:
         return self._lib.gpuhash_ndevices(self._ctx)
 
     def set_layout_policy(self, policy: int) -> None:
-        """LAYOUT_AUTO / LAYOUT_UNIFORM / LAYOUT_CLASSIC / LAYOUT_LANETABLE
-        (gpuhash_set_layout_policy)."""
+        """LAYOUT_AUTO / LAYOUT_UNIFORM / LAYOUT_CLASSIC / LAYOUT_LANETABLE, optionally OR
+        LAYOUT_TAIL_ALWAYS or LAYOUT_TAIL_NEVER (gpuhash_set_layout_policy)."""
         rc = self._lib.gpuhash_set_layout_policy(self._ctx, policy)
         if rc != GPUHASH_OK:
             raise GpuHashError(rc, "gpuhash_set_layout_policy")

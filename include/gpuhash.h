@@ -140,6 +140,17 @@ int gpuhash_shard_range(size_t msg_len, uint64_t lower, uint64_t upper, int nsha
 #define GPUHASH_LAYOUT_CLASSIC 2
 #define GPUHASH_LAYOUT_LANETABLE 3
 #define GPUHASH_LANETABLE_MAX 65536u
+/* Tail-digit launches, for any policy above: a digit group whose last
+ * digit-bearing word holds ONE digit after a word of four (e.g. "bradfitz" at 8 and 12
+ * digits) would loop over only 10 values per 256-lane row; it runs instead as ten
+ * launches, one per last digit t, over the nonces = t (mod 10) with t a constant message
+ * byte, looping over the previous word's 10^4 values.  Taken when the search spans at
+ * least GPUHASH_TAIL_MIN_SPAN nonces of the group (below that, the launches' partial rows
+ * cost more than the short loop); OR GPUHASH_LAYOUT_TAIL_ALWAYS or _NEVER into the policy
+ * to force either way (parity tests, tuning).  Results are identical either way. */
+#define GPUHASH_LAYOUT_TAIL_ALWAYS 16
+#define GPUHASH_LAYOUT_TAIL_NEVER 32
+#define GPUHASH_TAIL_MIN_SPAN 8589934592ull
 int gpuhash_set_layout_policy(gpuhash_ctx *ctx, int policy);
 
 /* argmin_{n in [lower, upper]} (Hash(msg, n), n) -> *out_hash, *out_nonce.

@@ -66,6 +66,31 @@ def test_hash_range_bit_exact(engine, oracle):
         assert bad.size == 0, (len(m), lo, cnt, int(bad[0]) + lo)
 
 
+@pytest.mark.parametrize("mlen,d,j", [
+    (8, 12, 4), (8, 8, 3), (12, 12, 5), (27, 9, 8),     # plain: last word = 1 digit
+    (42, 14, 13), (46, 14, 14), (42, 18, 14),           # the extra-padding-block kernels
+])
+def test_tail_digit_launches(engine, oracle, mlen, d, j, request):
+    """Tail-digit launches (include/gpuhash.h), forced on small ranges:
+    per-nonce parity across the last-digit residues, the loop word's roll-overs and the
+    lane rows (the kernel maps k back to nonce = 10 k + t), and min parity, on the J-1
+    kernel the layout moves the group to."""
+    import gpuhash
+    request.addfinalizer(lambda: engine.set_layout_policy(gpuhash.LAYOUT_AUTO))
+    engine.set_layout_policy(gpuhash.LAYOUT_AUTO | gpuhash.LAYOUT_TAIL_ALWAYS)
+    rng = random.Random(mlen * 100 + d)
+    m = bytes(rng.randrange(32, 127) for _ in range(mlen))
+    base = 10 ** (d - 1) + rng.randrange(10 ** (d - 2))
+    for lo in (base - base % 10 ** 5 - 4321, base + 7):
+        got = engine.hash_range(m, lo, 60000)
+        assert {(r["J"], r["digits"]) for r in engine.launches()} == {(j, d)}, engine.launches()
+        want = oracle.hash_range(m, lo, 60000)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (mlen, d, lo, int(bad[0]) + lo if bad.size else None)
+    for lo, hi in ((base, base + 400_000), (base - base % 10 ** 6 - 13, base - base % 10 ** 6 + 250_000)):
+        assert engine.min(m, lo, hi) == oracle.min(m, lo, hi, threads=16), (mlen, d, lo, hi)
+
+
 @pytest.mark.parametrize("mlen,d,c2,j", [
     (58, 10, 2, 1), (59, 10, 2, 1), (60, 10, 2, 1), (56, 12, 2, 1), (59, 12, 2, 1),  # two-word loop
     (120, 10, 1, 0), (54, 10, 1, 0), (119, 12, 1, 0),                                # K+W table

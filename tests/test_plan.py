@@ -24,7 +24,8 @@ u64 = ctypes.c_uint64
 class Info(ctypes.Structure):
     _fields_ = ([(n, ctypes.c_int) for n in "J C2 EX d q s".split()]
                 + [(n, u64) for n in "lo hi base".split()]
-                + [(n, ctypes.c_uint32) for n in "nblocks R rchunk nrchunks p_first p_last r_first r_last".split()])
+                + [(n, ctypes.c_uint32) for n in "nblocks R rchunk nrchunks p_first p_last r_first r_last".split()]
+                + [(n, ctypes.c_uint32) for n in "stride tail".split()])
 
 
 @pytest.fixture(scope="module")
@@ -55,6 +56,49 @@ def plan(hc, m, a, b, rchunk=0):
     return list(arr)
 
 
+def count(l):
+    """Nonces of launch l (a tail-digit launch covers every stride-th nonce of [lo, hi])."""
+    return (l.hi - l.lo) // l.stride + 1
+
+
+def some_nonce(rng, l):
+    return l.lo + l.stride * rng.randrange(count(l))
+
+
+def assert_tiles(p, a, b):
+    """The launches cover [a, b] exactly once, in order: plain launches tile it, and each
+    run of tail-digit launches (one digit group) covers its span [A, B] as ten residue
+    classes, class t's k = nonce / 10 ranges tiling [ceil((A-t)/10), floor((B-t)/10)]."""
+    i, nxt = 0, a
+    while i < len(p):
+        l = p[i]
+        if l.stride == 1:
+            assert l.lo == nxt, (i, l.lo, nxt)
+            nxt = l.hi + 1
+            i += 1
+            continue
+        j = i
+        while j < len(p) and p[j].stride != 1 and p[j].d == l.d:
+            j += 1
+        run = p[i:j]
+        A, B = nxt, max(x.hi for x in run)
+        assert min(x.lo for x in run) >= A and B <= b
+        for t in range(10):
+            ks = sorted(((x.lo - t) // 10, (x.hi - t) // 10) for x in run if x.tail == t)
+            assert all(x.lo % 10 == t and x.hi % 10 == t and x.stride == 10 for x in run if x.tail == t)
+            ka, kb = (A - t + 9) // 10 if A > t else 0, (B - t) // 10
+            if ka > kb:
+                assert not ks
+                continue
+            assert ks and ks[0][0] == ka and ks[-1][1] == kb, (t, ks, ka, kb)
+            for (x0, x1), (y0, y1) in zip(ks, ks[1:]):
+                assert y0 == x1 + 1
+        assert sum(count(x) for x in run) == B - A + 1
+        nxt = B + 1
+        i = j
+    assert nxt == b + 1
+
+
 def desc_hash(hc, m, a, b, i, n, rchunk=0):
     o = u64()
     assert hc.hostcheck_desc_hash(m, len(m), a, b, rchunk, i, n, ctypes.byref(o)) == 0
@@ -68,9 +112,7 @@ def test_plan_tiles_range_and_layouts_are_legal(hc):
         a = rng.randrange(0, U64)
         b = min(U64, a + rng.randrange(0, 10 ** rng.randrange(0, 13)))
         p = plan(hc, m, a, b)
-        assert p[0].lo == a and p[-1].hi == b
-        for x, y in zip(p, p[1:]):
-            assert y.lo == x.hi + 1
+        assert_tiles(p, a, b)
         for l in p:
             if l.C2 == 3:  # lane table: lanes = W_0/W_1 digits, loop = block B-1 digits
                 assert l.J == 1 and 5 <= l.q <= 8 and 1 <= l.s <= 8 and not l.EX
@@ -88,8 +130,10 @@ def test_plan_tiles_range_and_layouts_are_legal(hc):
                 assert 1 <= l.q <= 4 and 0 <= l.s <= 8 and l.s + l.q <= 10
             assert not (l.C2 and l.J > 1) and not (l.EX and l.J < 13) and not (l.C2 and l.EX)
             assert l.R == 10 ** l.q
-            assert l.lo == l.base + l.p_first * l.R + l.r_first
-            assert l.hi == l.base + l.p_last * l.R + l.r_last
+            assert (l.lo - l.tail) // l.stride == l.base + l.p_first * l.R + l.r_first
+            assert (l.hi - l.tail) // l.stride == l.base + l.p_last * l.R + l.r_last
+            if l.stride != 1:  # tail-digit launch: plain, the loop word's four digits
+                assert l.stride == 10 and l.q == 4 and not l.C2 and l.tail < 10
             assert l.nblocks == ((l.p_last - l.p_first) // 256 + 1) * l.nrchunks
             assert l.nrchunks * l.rchunk >= l.R
 
@@ -108,7 +152,7 @@ def test_descriptor_replay_matches_oracle(hc, oracle, policy):
         b = min(hi, a + rng.randrange(0, 10 ** rng.randrange(0, 12)))
         for i, l in enumerate(plan(hc, m, a, b)):
             seen.add((l.J, l.C2, l.EX))
-            for n in {l.lo, l.hi, rng.randrange(l.lo, l.hi + 1)}:
+            for n in {l.lo, l.hi, some_nonce(rng, l)}:
                 assert desc_hash(hc, m, a, b, i, n) == oracle.hash(m, n), (m, a, b, i, n)
     hc.hostcheck_set_layout_policy(AUTO)
     # the reachable (J, C2, EX) variants of each policy were all exercised: 14 plain, 3
@@ -212,8 +256,8 @@ def test_long_messages(hc, oracle, mlen):
 def test_wide_ranges_plan(hc):
     for a, b in [(0, (1 << 40) - 1), (0, (1 << 32) - 1), (U64 - 10 ** 12, U64)]:
         p = plan(hc, b"bradfitz", a, b)
-        assert p[0].lo == a and p[-1].hi == b
-        assert sum(l.hi - l.lo + 1 for l in p) == b - a + 1
+        assert_tiles(p, a, b)
+        assert sum(count(l) for l in p) == b - a + 1
 
 
 def test_rchunk_override(hc, oracle):
@@ -265,10 +309,73 @@ def test_lane_table_straddles(hc, oracle, mlen):
             if b is None:
                 b = min(hi, a + rng.randrange(1, 10 ** 6))
             p = plan(hc, m, a, b)
-            assert p[0].lo == a and p[-1].hi == b
+            assert_tiles(p, a, b)
             for i, l in enumerate(p):
                 seen += l.C2 == 3
-                pts = {l.lo, l.hi, rng.randrange(l.lo, l.hi + 1)}
+                pts = {l.lo, l.hi, some_nonce(rng, l)}
                 for n in pts:
                     assert desc_hash(hc, m, a, b, i, n) == oracle.hash(m, n), (mlen, d, a, b, i, n)
     assert seen > 0
+
+
+TAIL_ALWAYS, TAIL_NEVER = 16, 32
+
+
+def test_tail_digit_layouts_replay(hc, oracle):
+    """Tail-digit launches (include/gpuhash.h): with the last digit fixed
+    per launch, every launch of every qualifying digit group -- message lengths 0-129, so
+    the one-digit last word lands in every word position and block, extra padding block
+    included -- replays bit-exact against the oracle, and the ten residue classes tile
+    the range."""
+    rng = random.Random(37)
+    hc.hostcheck_set_layout_policy(AUTO | TAIL_ALWAYS)
+    try:
+        tails, variants = 0, set()
+        for mlen in range(0, 130):
+            m = bytes(rng.randrange(256) for _ in range(mlen))
+            for d in range(6, 21):
+                lo_d, hi_d = 10 ** (d - 1), min(10 ** d - 1, U64)
+                a = rng.randrange(lo_d, hi_d + 1)
+                b = min(hi_d, a + rng.randrange(0, 10 ** rng.randrange(1, 6)))
+                p = plan(hc, m, a, b)
+                assert_tiles(p, a, b)
+                for i, l in enumerate(p):
+                    if l.stride == 1:
+                        continue
+                    tails += 1
+                    variants.add((l.J, l.EX))
+                    for n in {l.lo, l.hi, some_nonce(rng, l)}:
+                        assert desc_hash(hc, m, a, b, i, n) == oracle.hash(m, n), (mlen, a, b, i, n)
+        assert tails > 1000 and (13, 1) in variants and (14, 1) in variants, (tails, sorted(variants))
+    finally:
+        hc.hostcheck_set_layout_policy(AUTO)
+
+
+def test_tail_digit_span_rule(hc):
+    """AUTO takes the tail-digit launches only for a digit group the search spans
+    GPUHASH_TAIL_MIN_SPAN (2^33) nonces of; the flags force either way."""
+    import re
+    h = open(os.path.join(ROOT, "include", "gpuhash.h")).read()
+    assert int(re.search(r"#define GPUHASH_TAIL_MIN_SPAN (\d+)ull", h).group(1)) == 1 << 33
+    assert int(re.search(r"#define GPUHASH_LAYOUT_TAIL_ALWAYS (\d+)", h).group(1)) == TAIL_ALWAYS
+    assert int(re.search(r"#define GPUHASH_LAYOUT_TAIL_NEVER (\d+)", h).group(1)) == TAIL_NEVER
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "bitcoin-miner_amd"))
+    import gpuhash
+    assert (gpuhash.LAYOUT_TAIL_ALWAYS, gpuhash.LAYOUT_TAIL_NEVER, gpuhash.TAIL_MIN_SPAN) == (TAIL_ALWAYS, TAIL_NEVER, 1 << 33)
+    m = b"bradfitz"  # 12 digits: W_4 = 4 digits, W_5 = the 12th digit + 0x80
+    a = 10 ** 11
+    strides = lambda p: {l.stride for l in p}
+    assert strides(plan(hc, m, a, a + (1 << 33) - 2)) == {1}
+    p = plan(hc, m, a, a + (1 << 33) - 1)
+    assert strides(p) == {10} and {(l.J, l.q) for l in p} == {(4, 4)} and {l.tail for l in p} == set(range(10))
+    assert_tiles(p, a, a + (1 << 33) - 1)
+    # 10- and 11-digit bradfitz groups (3 and 4 digits in W_4) never qualify
+    assert strides(plan(hc, m, 10 ** 9, 10 ** 11 - 1)) == {1}
+    try:
+        hc.hostcheck_set_layout_policy(AUTO | TAIL_NEVER)
+        assert strides(plan(hc, m, 0, (1 << 40) - 1)) == {1}
+        hc.hostcheck_set_layout_policy(AUTO | TAIL_ALWAYS)
+        assert 10 in strides(plan(hc, m, a, a + 99))
+    finally:
+        hc.hostcheck_set_layout_policy(AUTO)

@@ -28,7 +28,8 @@ with gpuhash.Engine([0], lib_path=sys.argv[1]) as e:
              ("u2f", b"u" * 58, 10240 * 10**7, 10240 * 10**7 + 256 * 10**7 - 1),  # C2=2, one full row
              ("u2p", b"u" * 60, 10**9, (1 << 32) - 1),  # C2=2, 430 lane values: wave 3 of row 2 idle
              ("lt61", b"t" * 61, 10**9, 10**9 + (1 << 31)),        # C2=3 lane table, 2 digits in B-1
-             ("lt58", b"t" * 58, 10**11, 10**11 + (1 << 32))]     # C2=3 lane table, 5 digits in B-1
+             ("lt58", b"t" * 58, 10**11, 10**11 + (1 << 32)),     # C2=3 lane table, 5 digits in B-1
+             ("q1", b"bradfitz", 10**11, 10**11 + (1 << 34) - 1)]  # 12 digits: one in the last word (tail-digit launches)
     only = os.environ.get("VCASES")
     if only:
         cases = [next(c for c in cases if c[0] == n) for n in only.split(",")]
