@@ -3,7 +3,8 @@
 
 Draws (message, range) cases across message lengths 0-300 (plus a few 1-4 KB), every
 digit count 1-20, ranges of 1 to ~2e6 nonces placed at random or straddling a digit-count
-boundary, under every layout policy, and compares gpuhash_min with the C oracle's scan.
+boundary, under every layout policy (a third of the cases with the tail-digit launches
+forced), and compares gpuhash_min with the C oracle's scan.
 Prints one JSON line per 100 cases and a summary; exits 1 on the first mismatch.
 """
 import json
@@ -51,6 +52,10 @@ with gpuhash.Engine([0]) as eng:
         m, lo, hi = case()
         policy = rng.choice([gpuhash.LAYOUT_AUTO, gpuhash.LAYOUT_UNIFORM, gpuhash.LAYOUT_CLASSIC,
                              gpuhash.LAYOUT_LANETABLE])
+        # round 4: the tail-digit launches (AUTO takes them only above 2^33 nonces per
+        # digit group, far beyond a soak case) forced on a third of the cases
+        if rng.random() < 1 / 3:
+            policy |= gpuhash.LAYOUT_TAIL_ALWAYS
         eng.set_layout_policy(policy)
         got = eng.min(m, lo, hi)
         want = oracle.min(m, lo, hi, threads=threads)
