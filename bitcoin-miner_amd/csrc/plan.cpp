@@ -449,6 +449,10 @@ void plan_range(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper
 
 double group_cost(uint64_t msg_len, int d) {
     GroupLayout g = layout_for(msg_len, d);
+    // a whole digit group spans far more than kTailMinSpan nonces: a one-digit last word
+    // runs as tail-digit launches, whose loop is the previous word's 10^4 values
+    GroupLayout gt;
+    if (tail_layout(msg_len, d, g, gt)) g = gt;
     // relative VALU work per nonce: one final-block compression, +0.7 for the extra
     // constant block, + the per-lane block B-1 compression amortised over R nonces.
     // (measured per-layout rates, profiles/r01_layout_sweep.jsonl: plain 32-39 GH/s,
