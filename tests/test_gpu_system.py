@@ -217,6 +217,10 @@ def test_config5_full_size(procs, engine, oracle, golden):
     port = free_port()
     drops = dict(LSPNET_CLIENT_READ_DROP=10, LSPNET_CLIENT_WRITE_DROP=10,
                  LSPNET_SERVER_READ_DROP=10, LSPNET_SERVER_WRITE_DROP=10)
+    # 200 ms epochs as in the other tests, but 25 of them (5 s, still half the reference's
+    # default 2 s x 5) before a connection counts as lost: 25 processes share the box's CPU
+    # share here, and one round-4 run lost a client after 2 s (10 epochs) of silence
+    drops = dict(drops, LSP_EPOCH_LIMIT=25)
     server = procs.start([os.path.join(BIN, "server"), str(port)], env=env(GPUHASH_SERVER_LOG=1, **drops))
     time.sleep(0.5)
     miners = [procs.start([os.path.join(BIN, "miner"), f"127.0.0.1:{port}"], env=env(**drops))
@@ -231,6 +235,11 @@ def test_config5_full_size(procs, engine, oracle, golden):
     miners[1].send_signal(signal.SIGKILL)  # mid-job (2^34-nonce jobs take ~4 s per miner here)
     outs = [c.communicate(timeout=400)[0].strip() for c in clients]
     wall = _t.time() - t0
+    if any(not o.startswith("Result") for o in outs):  # show the server's account of it
+        server.send_signal(signal.SIGTERM)
+        log = server.communicate(timeout=30)[1]
+        raise AssertionError(f"clients {[i for i, o in enumerate(outs) if not o.startswith('Result')]} "
+                             f"did not get a Result; server log tail:\n{log[-4000:]}")
     checked_golden = 0
     for i, out in enumerate(outs):
         parts = out.split()
