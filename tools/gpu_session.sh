@@ -2,7 +2,7 @@
 # tools/gpu_session.sh STEP... -- runs GPU steps on the gpurun box, each under its own
 # time limit, logging to gpurun_out/.  A plain failure (exit 1, e.g. a failing test)
 # lets the next step run; a fault, abort, segfault, time limit or kill stops the session.
-# Steps: inproc8s | dist8s | fma | cumask | family | inproc8c4 | valu | go | test | soak | smoke | bench | bench3 | bench4 | prof4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | pmc3 | pmc4 | sweep | variants | partial | regret | sys5
+# Steps: lsweep | inproc8s | dist8s | fma | cumask | family | inproc8c4 | valu | go | test | soak | smoke | bench | bench3 | bench4 | prof4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | pmc3 | pmc4 | sweep | variants | partial | regret | sys5
 set -u
 cd "$(dirname "$0")/.."
 OUT=gpurun_out
@@ -47,6 +47,7 @@ for step in "$@"; do
         latency) run latency 120 python -u tools/latency.py ;;
         ranks) run ranks 300 python -u tools/rank_windows.py --ranks "${RANKS:-0,1,2,3,4,5,6,7}" ;;
         sweep) run sweep 600 python -u tools/layout_sweep.py ;;
+        lsweep) run lsweep 900 python -u tools/length_sweep.py ;;
         regret) run regret 600 python -u tools/planner_regret.py ;;
         partial) run partial 600 python -u tools/partial_row_probe.py "${VROUNDS:-2}" "${VARIANTS:-old,new}" ;;
         variants) run variants 600 python -u tools/variant_bench.py "${VROUNDS:-3}" "${VARIANTS:-old,new}" ;;
