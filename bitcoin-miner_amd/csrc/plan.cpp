@@ -396,7 +396,8 @@ void plan_range(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper
             // 10) of [a, b] (a >= 10^(d-1) >= 10, so every k has d-1 digits)
             for (uint32_t t = 0; t < 10; t++) {
                 if (b < t) continue;
-                const uint64_t ka = a <= t ? 0 : (a - t + 9) / 10, kb = (b - t) / 10;
+                // ceil((a - t) / 10) without overflowing at a = 2^64-1
+                const uint64_t ka = a <= t ? 0 : (a - t) / 10 + ((a - t) % 10 != 0), kb = (b - t) / 10;
                 if (ka > kb) continue;
                 const uint64_t Uk = pow10u(gt.s + gt.q);
                 for (uint64_t H = ka / Uk;; H++) {

@@ -347,6 +347,14 @@ def test_tail_digit_layouts_replay(hc, oracle):
                     for n in {l.lo, l.hi, some_nonce(rng, l)}:
                         assert desc_hash(hc, m, a, b, i, n) == oracle.hash(m, n), (mlen, a, b, i, n)
         assert tails > 1000 and (13, 1) in variants and (14, 1) in variants, (tails, sorted(variants))
+        # the top of the uint64 range (ceil((a - t) / 10) must not overflow at a = 2^64-1)
+        for m in (b"", b"bradfitz", b"x" * 42):
+            for a, b in ((U64 - 5, U64), (U64, U64), (U64 - 123456, U64 - 17)):
+                p = plan(hc, m, a, b)
+                assert_tiles(p, a, b)
+                for i, l in enumerate(p):
+                    for n in {l.lo, l.hi}:
+                        assert desc_hash(hc, m, a, b, i, n) == oracle.hash(m, n), (m, a, b, i, n)
     finally:
         hc.hostcheck_set_layout_policy(AUTO)
 
