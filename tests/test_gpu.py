@@ -91,6 +91,21 @@ def test_tail_digit_launches(engine, oracle, mlen, d, j, request):
         assert engine.min(m, lo, hi) == oracle.min(m, lo, hi, threads=16), (mlen, d, lo, hi)
 
 
+def test_tail_digit_launches_top_of_u64(engine, oracle, request):
+    """Tail-digit launches at 20 digits up to 2^64-1 (nonce = 10 k + t at the top of the
+    uint64 range), per nonce and min, against the oracle."""
+    import gpuhash
+    request.addfinalizer(lambda: engine.set_layout_policy(gpuhash.LAYOUT_AUTO))
+    engine.set_layout_policy(gpuhash.LAYOUT_AUTO | gpuhash.LAYOUT_TAIL_ALWAYS)
+    for m in (b"", b"bradfitz"):  # 20 digits end W_5 / W_7 byte 0: one digit in the last word
+        lo = U64 - 59999
+        got = engine.hash_range(m, lo, 60000)
+        assert {r["digits"] for r in engine.launches()} == {20}
+        assert (got == oracle.hash_range(m, lo, 60000)).all()
+        for a, b in ((U64 - 5, U64), (U64, U64), (U64 - 300_000, U64 - 17)):
+            assert engine.min(m, a, b) == oracle.min(m, a, b), (m, a, b)
+
+
 @pytest.mark.parametrize("mlen,d,c2,j", [
     (58, 10, 2, 1), (59, 10, 2, 1), (60, 10, 2, 1), (56, 12, 2, 1), (59, 12, 2, 1),  # two-word loop
     (120, 10, 1, 0), (54, 10, 1, 0), (119, 12, 1, 0),                                # K+W table
