@@ -86,24 +86,10 @@ __device__ __forceinline__ uint32_t bs1(uint32_t x) { return xor3(rotr(x, 17), r
 
 // Wave-uniform primitives: plain C so the compiler keeps them on SALU.
 __device__ __forceinline__ uint32_t urotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
-#ifdef GPUHASH_SALU_SIGMA
-// Tuning hook (tools/build_fold_variants.sh, off in the product build): LLVM turns the
-// uniform sigma0(W_J) into v_alignbit with SGPR sources (VALU); this pins it on SALU as
-// the low word of the 64-bit shift of the pair {x, x}.  Measured 2.6% SLOWER on config
-// 2 (profiles/r04_fold_variants.jsonl).
-template <int N>
-__device__ __forceinline__ uint32_t srotr(uint32_t x) {
-    const unsigned long long p = ((unsigned long long)x << 32) | x;
-    unsigned long long r;
-    asm("s_lshr_b64 %0, %1, %2" : "=s"(r) : "s"(p), "i"(N));
-    return (uint32_t)r;
-}
-__device__ __forceinline__ uint32_t us0(uint32_t x) { return srotr<7>(x) ^ srotr<18>(x) ^ (x >> 3); }
-__device__ __forceinline__ uint32_t us1(uint32_t x) { return srotr<17>(x) ^ srotr<19>(x) ^ (x >> 10); }
-#else
+// (LLVM issues the uniform sigma0(W_J) as v_alignbit with SGPR sources; pinning it on
+// SALU measured 2.6% slower on config 2: tools/tuning_hooks.patch)
 __device__ __forceinline__ uint32_t us0(uint32_t x) { return urotr(x, 7) ^ urotr(x, 18) ^ (x >> 3); }
 __device__ __forceinline__ uint32_t us1(uint32_t x) { return urotr(x, 17) ^ urotr(x, 19) ^ (x >> 10); }
-#endif
 
 __device__ __forceinline__ uint32_t ascii4(uint32_t x) {
     uint32_t x1 = x / 10u, x2 = x1 / 10u, x3 = x2 / 10u;
@@ -146,8 +132,8 @@ __device__ __forceinline__ void round_kw(State& s, uint32_t kw) {
 // reads `kw` in the 2-input h + kw.  Here it goes into the 3-input add, slow class
 // anyway, so the round's 2-input adds read VGPRs only.  The K+W-table layout (config 3)
 // runs +1.8% with it; the plain, extra-block and lane-table rounds with a uniform K+W run
-// 0.3-3.8% SLOWER with it (tuning hooks GPUHASH_FOLD_{PLAIN,EX,LT}, off in the product
-// build; profiles/r04_fold_variants.jsonl), so only ut_hash's table rounds use it.
+// 0.3-3.8% SLOWER with it (tools/tuning_hooks.patch; profiles/r04_fold_variants.jsonl),
+// so only ut_hash's table rounds use it.
 __device__ __forceinline__ void round_ukw(State& s, uint32_t kw) {
     uint32_t x;
     asm("v_add3_u32 %0, %1, %2, %3" : "=v"(x) : "v"(s.h), "s"(kw), "v"(ch(s.e, s.f, s.g)));
@@ -390,26 +376,10 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
                 x.h = x.g; x.g = x.f; x.f = x.e; x.e = (x.d + inv) + WJ;
                 x.d = x.c; x.c = x.b; x.b = x.a; x.a = (inv + t2) + WJ;
             }
-#ifdef GPUHASH_EXTRA_SALU
-            // tuning probe (tools/build_salu_variants.sh, never in the product build): one
-            // extra scalar instruction per round from round 20 on -- as many as the K
-            // constants the loop re-materialises with s_mov_b32 -- to price those s_movs
-            uint32_t salu_dummy = __builtin_amdgcn_readfirstlane(r);
-#endif
             sfor<J + 1, 63>([&](auto tc) {
                 constexpr int t = decltype(tc)::value;
-#ifdef GPUHASH_EXTRA_SALU
-                if constexpr (t >= 20) asm volatile("s_xor_b32 %0, %0, %1" : "+s"(salu_dummy) : "i"(K[t]));
-#endif
                 if constexpr (t < 16) {
-#ifdef GPUHASH_FOLD_PLAIN
-                    // tuning hook (round_ukw above; 3% slower on config 2): h = e_{t-3} is
-                    // per-lane from round J+2 on (C2 = 0: rounds before J-2 are the host's)
-                    if constexpr (C2 == 0 && t >= J + 2) round_ukw(x, K[t] + w[t]);
-                    else round_kw(x, K[t] + w[t]);
-#else
                     round_kw(x, K[t] + w[t]);   // uniform word: K+W folds
-#endif
                 } else {
                     sched(tc);
                     round_kw(x, w[t] + K[t]);
@@ -428,11 +398,7 @@ __device__ __forceinline__ void scan_row(const LaunchDesc& D, uint32_t row, uint
                 const uint32_t y0 = y.a, y1 = y.b;
                 sfor<0, 63>([&](auto tc) {
                     constexpr int t = decltype(tc)::value;
-#ifdef GPUHASH_FOLD_EX
-                    round_ukw(y, D.KWX[t]);   // tuning hook (round_ukw above): no gain
-#else
                     round_kw(y, D.KWX[t]);
-#endif
                 });
                 uint32_t t1 = y.h + D.KWX[63] + ch(y.e, y.f, y.g) + bS1(y.e);
                 H0 = y0 + t1 + bS0(y.a) + maj(y.a, y.b, y.c);
@@ -474,21 +440,13 @@ __device__ __forceinline__ void scan_row_lt(const LaunchDesc& D, uint32_t row, u
     }
 #pragma unroll 1
     for (uint32_t r = r0; r < r1; r++) {
-#ifdef GPUHASH_LT_ALIGN
-        GPUHASH_LOOP_ALIGN();
-#endif
         const uint32_t* __restrict__ P = ptab + D.tab_off + 16u * r;
         uint32_t cv[8];
 #pragma unroll
         for (int i = 0; i < 8; i++) cv[i] = P[i];
         const State s{cv[0], cv[1], cv[2], cv[3], cv[4], cv[5], cv[6], cv[7]};
         uint32_t H0, H1;
-        // kw[2..15] = K + the message's constant words (uniform); h is per-lane from round 4
-#ifdef GPUHASH_FOLD_LT  // tuning hook (round_ukw above): 3.8% slower
-        ut_hash<4, 16>(s, cv, P[8], P[9], [&](int t) { return kw[t]; }, H0, H1);
-#else
         ut_hash<0, 0>(s, cv, P[8], P[9], [&](int t) { return kw[t]; }, H0, H1);
-#endif
 #ifdef GPUHASH_TIE_TEST_BITS
         H0 >>= (32 - GPUHASH_TIE_TEST_BITS);
         H1 = 0;

@@ -110,3 +110,49 @@ def test_hot_loops_start_at_4_mod_8(tmp_path):
         pins = [p for p in pinned_runs(co, kernel) if p is not None]
         assert len(pins) == 1, (tu, kernel, pins)   # exactly the per-nonce loop body
         assert pins[0] % 8 == 4, (tu, kernel, hex(pins[0]))
+
+
+def test_kernel_source_has_no_tuning_hooks():
+    """The measured-negative tuning hooks of round 4 live in tools/tuning_hooks.patch, not
+    in the product kernel source: the only conditionals left in
+    scan_kernel.h are the loop-phase pin, the tie-test build and the waves-per-SIMD
+    attribute the Makefile sets for the plain kernels."""
+    src = open(os.path.join(PKG, "csrc", "scan_kernel.h")).read()
+    conds = re.findall(r"^\s*#\s*(?:if|ifdef|ifndef|elif)\b(.*)$", src, re.M)
+    allowed = ("GPUHASH_LOOP_PHASE", "GPUHASH_TIE_TEST_BITS", "GPUHASH_WAVES_PER_EU")
+    assert conds and all(any(a in c for a in allowed) for c in conds), conds
+    for hook in ("SALU_SIGMA", "FOLD_PLAIN", "FOLD_EX", "FOLD_LT", "EXTRA_SALU", "LT_ALIGN"):
+        assert "GPUHASH_" + hook not in src
+    patch = open(os.path.join(ROOT, "tools", "tuning_hooks.patch")).read()
+    assert all("GPUHASH_" + h in patch for h in ("SALU_SIGMA", "FOLD_PLAIN", "EXTRA_SALU", "LT_ALIGN"))
+
+
+def test_config2_kernel_code_is_the_measured_one(tmp_path):
+    """The config-2 search kernel (J = 4, plain) as profiled in round 4: 64 VGPRs, no
+    spills, and a per-nonce loop body of 1,271 instructions (1,196 VALU, 75 SALU; PMC
+    counted 1,197.9 VALU per nonce, profiles/r04e_pmc_summary.json).  Removing the tuning
+    hooks left the machine code byte-identical; this keeps it from drifting unnoticed."""
+    if not (shutil.which("objcopy") and os.path.exists(os.path.join(LLVM, "llvm-objdump"))):
+        pytest.skip("binutils / ROCm LLVM tools not present")
+    obj = os.path.join(PKG, "build", "kernels_plain.o")
+    if not os.path.exists(obj):
+        subprocess.check_call(["make", "-s", "-C", PKG, "build/kernels_plain.o"])
+    meta = kernel_metadata(obj, tmp_path)
+    k4 = [v for n, v in meta.items() if "k_scanILi4ELi0ELb0ELi0E" in n]
+    assert k4 == [(64, 0)], k4
+    d = subprocess.check_output([os.path.join(LLVM, "llvm-objdump"), "-d", str(tmp_path / "k.co")], text=True)
+    kern = "_ZN7gpuhash6k_scanILi4ELi0ELb0ELi0EE"
+    i = d.index("<" + kern)
+    body = d[i:d.index("s_endpgm", i)]
+    runs, cur = [], []
+    for line in body.split("\n"):
+        m = re.match(r"\s+([vs]_\S+|global_\S+|scratch_\S+|ds_\S+|buffer_\S+|flat_\S+)\s.*//\s*[0-9A-Fa-f]+:", line)
+        if not m:
+            continue
+        cur.append(m.group(1))
+        if m.group(1).startswith(("s_cbranch", "s_branch")):
+            runs.append(cur)
+            cur = []
+    loops = [(len(r), sum(op.startswith("v_") for op in r), sum(op.startswith("s_") for op in r))
+             for r in runs if sum(op.startswith("v_") for op in r) >= 500]
+    assert loops == [(1271, 1196, 75)], loops

@@ -17,6 +17,7 @@ TMP=$(mktemp -d)
 trap 'rm -rf "$TMP"' EXIT
 mkdir -p "$TMP/bitcoin-miner_amd"
 cp -r bitcoin-miner_amd/csrc "$TMP/bitcoin-miner_amd/csrc"
+patch -s -p1 -d "$TMP" < tools/tuning_hooks.patch  # sched_ahead.patch is written against it
 patch -s -p1 -d "$TMP" < tools/sched_ahead.patch
 INC="-Iinclude -I$TMP/bitcoin-miner_amd/csrc"
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC $INC -Wno-unused-result -Wno-unused-value -DGPUHASH_WAVES_PER_EU=8"
