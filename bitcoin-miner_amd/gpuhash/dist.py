@@ -1,4 +1,6 @@
-"""gpuhash.dist -- one process per GPU over torch.distributed (RCCL on ROCm, gloo on CPU).
+"""gpuhash.dist -- one process per GPU over torch.distributed, gloo by default (a host-side
+TCP merge of 24-byte results; no RCCL on the data path -- bench.py's GPUHASH_DIST_BACKEND=nccl
+moves only the barrier and merge onto RCCL).
 
 The nonce search partitions perfectly: nonces are independent and the reduction is one
 associative argmin over the lexicographic (hash, nonce) key.  So ranks

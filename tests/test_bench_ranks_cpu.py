@@ -26,7 +26,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, ndev, share, q):
+def _worker(rank, world, port, ndev, share, q, pinned=False):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "bitcoin-miner_amd"))
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -34,6 +34,8 @@ def _worker(rank, world, port, ndev, share, q):
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     if share:
         os.environ["GPUHASH_SHARE_GPU"] = "1"
+    if pinned:  # the launcher gave each rank one visible GPU: every rank sees ordinal 0
+        os.environ["HIP_VISIBLE_DEVICES"] = str(rank)
     import torch
     import gpuhash
     import hash_oracle
@@ -74,7 +76,9 @@ def _worker(rank, world, port, ndev, share, q):
             pass
 
     gpuhash.Engine = FakeEngine
-    props = lambda d: types.SimpleNamespace(pci_domain_id=0, pci_bus_id=0x10 + 0x10 * d, pci_device_id=0)
+    # a physical GPU's PCI id: by ordinal, or by rank when each rank sees only its own GPU
+    props = lambda d: types.SimpleNamespace(pci_domain_id=0, pci_bus_id=0x10 + 0x10 * (rank if pinned else d),
+                                            pci_device_id=0)
     torch.cuda.device_count = lambda: ndev
     torch.cuda.set_device = lambda d: None
     torch.cuda.synchronize = lambda d=None: None
@@ -92,12 +96,12 @@ def _worker(rank, world, port, ndev, share, q):
     q.put((rank, code, out.getvalue()))
 
 
-def _run(ndev, share):
+def _run(ndev, share, pinned=False):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, ndev, share, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, ndev, share, q, pinned)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict((r, (c, o)) for r, c, o in (q.get(timeout=120) for _ in range(world)))
@@ -122,9 +126,27 @@ def test_two_ranks_on_two_gpus_search_leg_and_inproc_repeat():
     si = line["search_2p40_inproc"]
     assert si["matches_golden"] is True and si["devices"] == [0, 1]
     assert [x["device"] for x in si["shards"]] == [0, 1]
-    assert line["rank_devices"] == [{"rank": 0, "device": 0, "pci": "0000:10:00"},
-                                    {"rank": 1, "device": 1, "pci": "0000:20:00"}]
+    assert [(d["rank"], d["device"], d["pci"]) for d in line["rank_devices"]] == \
+        [(0, 0, "0000:10:00"), (1, 1, "0000:20:00")]
     assert "device_check" not in line
+    # same-run scaling evidence: rank 0's search window again, alone
+    sc = s["scaling"]
+    assert sc["shard"] == 0 and sc["windows"] == s["shards"][0]["windows"]
+    assert sc["t_all_s"] == s["seconds"] and sc["scaling_efficiency"] > 0
+    # the timed step spans [0, 2^33): no committed golden, so its check is skipped, with why
+    assert line["matches_golden"] is None and "no committed golden" in line["result_check"]["reason"]
+
+
+def test_ranks_pinned_to_one_visible_gpu_each():
+    """ranks launched with one visible GPU each all report ordinal 0; distinct
+    GPUs are judged by (host, PCI id), so a correct pinned run has no device_check."""
+    code, line = _run(ndev=1, share=False, pinned=True)
+    assert code in (0, None), line.get("device_check")
+    assert [d["device"] for d in line["rank_devices"]] == [0, 0]
+    assert len({d["pci"] for d in line["rank_devices"]}) == 2
+    assert "device_check" not in line
+    assert line["search_2p40"]["matches_golden"] is True
+    assert "search_2p40_inproc" not in line  # no rank can see every GPU
 
 
 def test_shared_gpu_rehearsal_repeats_ordinal_zero():

@@ -5,6 +5,7 @@ same inputs, at sizes the C oracle finishes in seconds; the committed golden fix
 (tests/golden/golden.json, incl. the full 2^32 config-2 range); and at full sizes
 through size-independent properties (split/merge invariance, winner re-hash).
 """
+import os
 import random
 
 import numpy as np
@@ -415,6 +416,65 @@ def test_distinct_devices(oracle, golden):
         _check_distinct_shards(recs, devs, g["lower"], g["upper"])
         assert {r["device"] for r in recs} == set(devs)  # every GPU took a shard
         assert multi.stats()["ndevices"] == n
+
+
+def _bench(args, env=None, timeout=300):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    e.update(env or {})
+    return subprocess.Popen([sys.executable, os.path.join(root, "bench.py"), *args], stdout=subprocess.PIPE,
+                            stderr=subprocess.PIPE, text=True, env=e, cwd=root)
+
+
+def test_distinct_devices_bench_inproc():
+    """bench.py's in-process path over every visible GPU (distinct
+    ordinals, one context), the search leg over config 2's [0, 2^32) against its golden,
+    with shards on distinct PCI devices and the same-run scaling field."""
+    import json
+    import gpuhash
+    n = gpuhash.device_count()
+    if n < 2:
+        pytest.skip(f"{n} HIP device visible: the distinct-device bench path needs >= 2")
+    p = _bench(["--gpus", str(n), "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--search", "0:2^32-1"])
+    out, err = p.communicate(timeout=300)
+    assert p.returncode == 0, err[-2000:]
+    line = json.loads(out.strip().splitlines()[-1])
+    s = line["search_2p40"]
+    assert s["golden_name"] == "cfg2_bradfitz_2p32" and s["matches_golden"] is True
+    assert [x["device"] for x in s["shards"]] == list(range(n))
+    assert len({x["pci"] for x in s["shards"]}) == n and "device_check" not in line
+    assert 0 < s["scaling"]["scaling_efficiency"] <= 1.2
+
+
+def test_distinct_devices_bench_ranks_one_visible_gpu_each():
+    """VERDICT r04 item 6 / ADVICE r04: one bench.py process per GPU, each started with
+    HIP_VISIBLE_DEVICES naming only its own GPU (every rank sees ordinal 0); distinct GPUs
+    are proven by PCI id, and the gloo-merged search over [0, 2^32) equals its golden."""
+    import json
+    import socket
+    import gpuhash
+    n = gpuhash.device_count()
+    if n < 2:
+        pytest.skip(f"{n} HIP device visible: one-GPU-per-rank launches need >= 2")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = [_bench(["--gpus", str(n), "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--search",
+                     "0:2^32-1"],
+                    env=dict(RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(n), LOCAL_WORLD_SIZE="1",
+                             MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HIP_VISIBLE_DEVICES=str(r)))
+             for r in range(n)]
+    outs = [p.communicate(timeout=300) for p in procs]
+    assert all(p.returncode == 0 for p in procs), [o[1][-1500:] for o in outs]
+    line = json.loads([x for x in outs[0][0].splitlines() if x.startswith("{")][-1])
+    assert [d["device"] for d in line["rank_devices"]] == [0] * n
+    assert len({d["pci"] for d in line["rank_devices"]}) == n and "device_check" not in line
+    s = line["search_2p40"]
+    assert s["golden_name"] == "cfg2_bradfitz_2p32" and s["matches_golden"] is True
 
 
 def test_more_shards_than_nonces(oracle):

@@ -108,6 +108,15 @@ def test_bench_inproc_two_shards_on_one_gpu(engine):
     assert [x["shard"] for x in sh] == [0, 1] and [x["slices"] for x in sh] == [2, 2]
     assert bench.tiles(sh, 0, (1 << 40) - 1) and sum(x["nonces"] for x in sh) == 1 << 40
     assert all(x["device"] == 0 and x["stream_device"] == [0] for x in sh)
+    # same-run scaling evidence: shard 0's windows again, alone.  Two shards sharing one GPU
+    # do not scale, so shard 0 alone takes about half the two-shard time
+    sc = s["scaling"]
+    assert sc["windows"] == sh[0]["windows"] and 0.3 < sc["scaling_efficiency"] < 0.8, sc
+    # the timed step's shard rates are per step, near the kernel rate
+    assert all(x["nonces_hashed"] == x["nonces"] for x in line["shards"])  # one step here
+    assert all(x["kernel_GHs"] > 5 for x in line["shards"])
+    # [0, 2^33) has no committed golden: the step check says it was skipped
+    assert line["matches_golden"] is None and "no committed golden" in line["result_check"]["reason"]
 
 
 def test_bench_gpus_above_visible_fails_loudly():
@@ -144,6 +153,7 @@ def test_bench_torchrun_two_ranks_on_one_gpu(engine):
     si = line["search_2p40_inproc"]
     assert si["matches_golden"] is True and si["devices"] == [0, 0]
     assert [x["shard"] for x in si["shards"]] == [0, 1] and bench.tiles(si["shards"], 0, (1 << 32) - 1)
+    assert 0.3 < s["scaling"]["scaling_efficiency"] < 0.8  # two ranks share the GPU
     # without GPUHASH_SHARE_GPU, two ranks on a 1-GPU box must fail loudly: refused at
     # start, or -- when a *_VISIBLE_DEVICES variable leaves each process one GPU, which
     # bench.py accepts as one GPU per rank -- by the PCI check once both ranks report the
@@ -153,4 +163,17 @@ def test_bench_torchrun_two_ranks_on_one_gpu(engine):
         r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu-baseline",
                     "--search", "0:4294967295"], launcher=launcher[:-1] + [str(_free_port())])
         assert r.returncode != 0
-        assert "LOCAL_RANK 1" in r.stderr or "share a PCI device" in r.stderr, r.stderr[-1500:]
+        assert "LOCAL_RANK 1" in r.stderr or "share a (host, PCI) device" in r.stderr, r.stderr[-1500:]
+
+
+def test_bench_default_line_checks_its_step(engine):
+    """The headline line at N = 1 (config 2, [0, 2^32)) compares its timed step's result with
+    the committed golden and reports per-shard rates per step."""
+    r = _bench(["--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--search", "off"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["matches_golden"] is True and line["result_check"]["golden_names"] == ["cfg2_bradfitz_2p32"]
+    (sh,) = line["shards"]
+    assert sh["nonces"] == 1 << 32 and sh["nonces_hashed"] == 2 << 32
+    assert sh["kernel_GHs"] == pytest.approx(line["per_device"][0]["kernel_GHs"], rel=1e-3)
+    assert sh["kernel_GHs"] > 20 and 1500 < sh["sclk_mhz"] < 2600
