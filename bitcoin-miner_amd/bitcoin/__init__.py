@@ -8,11 +8,15 @@ miner (the GPU hot path), client.
 """
 from __future__ import annotations
 
-import json
 import os
-import re
 
 import lsp
+from gojson import LONE_SURROGATE as _LONE_SURROGATE
+from gojson import IntLit as _IntLit
+from gojson import field as _field
+from gojson import go_object, go_utf8  # noqa: F401 (re-exported for the tests)
+from gojson import loads as _go_loads
+from gojson import u64 as _u64
 from gpuhash import Hash, Message, MsgType, NewJoin, NewRequest, NewResult
 
 __all__ = ["Hash", "Message", "MsgType", "NewJoin", "NewRequest", "NewResult", "marshal",
@@ -72,89 +76,11 @@ def marshal(m: Message) -> bytes:
                            for k, v in d.items()) + "}").encode()
 
 
-_FOLD = str.maketrans("ABCDEFGHIJKLMNOPQRSTUVWXYZ", "abcdefghijklmnopqrstuvwxyz")
-
-
-class _Members(list):
-    """Every value one struct field received, in document order (go_object)."""
-
-
-def go_object(pairs) -> dict:
-    """json.loads object hook with encoding/json's field matching: a key selects the
-    struct field whose name equals it ignoring (ASCII) case.  Go decodes EVERY such member
-    in order into the field, so all of them are kept (case-folded key -> _Members): a later
-    null leaves the field as an earlier member set it, and a member of the wrong type fails
-    the message even when a later one is fine (csrc/lsp_native.h jfields)."""
-    out: dict = {}
-    for k, v in pairs:
-        out.setdefault(k.translate(_FOLD), _Members()).append(v)
-    return out
-
-
-def _field(d: dict, key: str, ok, default):
-    """The value json.Unmarshal leaves in field `key`: each matching member in order,
-    null skipped, the last accepted one wins; `ok(v)` False for any member -> ValueError
-    (Go keeps the first UnmarshalTypeError and returns it)."""
-    val = default
-    for v in d.get(key.translate(_FOLD), ()):
-        if v is None:
-            continue
-        if not ok(v):
-            raise ValueError(f"json: cannot unmarshal {v!r} into Go struct field Message.{key}")
-        val = v
-    return val
-
-
-class _IntLit(int):
-    """A JSON integer literal that keeps its text: Go's strconv.ParseUint refuses "-0",
-    which int() reads as 0."""
-
-    def __new__(cls, text: str):
-        o = int.__new__(cls, int(text))
-        o.text = text
-        return o
-
-
-def _u64(d: dict, key: str) -> int:
-    """A uint64 field as Go's json.Unmarshal accepts it: an integer literal in
-    [0, 2^64-1] (no fraction, exponent or sign); anything else fails the whole message."""
-    return int(_field(d, key, lambda v: isinstance(v, _IntLit) and not v.text.startswith("-")
-                      and v <= UINT64_MAX, 0))
-
-
-_LONE_SURROGATE = re.compile("[\ud800-\udfff]")
-
-
-def _go_replace(err: UnicodeDecodeError):
-    """utf-8 decode error handler with Go's utf8.DecodeRune rule: ONE U+FFFD per invalid
-    byte, decoding resumes at the next byte (Python's 'replace' emits one U+FFFD for a
-    whole truncated sequence: b'\xe2\x82A' -> '\ufffdA' where Go gives '\ufffd\ufffdA')."""
-    return "\ufffd", err.start + 1
-
-
-import codecs  # noqa: E402
-
-codecs.register_error("go-utf8", _go_replace)
-
-
-def go_utf8(raw: bytes) -> str:
-    """bytes -> str as Go's JSON decoder reads string contents: invalid UTF-8 (truncated or
-    overlong sequences, encoded surrogates, stray continuation bytes) as U+FFFD per byte."""
-    return bytes(raw).decode("utf-8", "go-utf8")
-
-
-def _not_json(name: str):
-    raise ValueError(f"invalid character in JSON: {name}")
-
-
 def unmarshal(raw: bytes) -> Message:
     """json.Unmarshal into bitcoin.Message (message.go:16-21); raises ValueError where Go
     would return an error, so callers drop the message as the reference would."""
-    if isinstance(raw, (bytes, bytearray)):
-        # Go's decoder turns invalid UTF-8 into U+FFFD instead of failing the message
-        raw = go_utf8(raw)
-    d = json.loads(raw, object_pairs_hook=go_object, parse_int=_IntLit,
-                   parse_constant=_not_json)  # NaN / Infinity: not JSON, Go refuses them
+    # invalid UTF-8 becomes U+FFFD (Go does not fail the message); NaN / Infinity are refused
+    d = _go_loads(raw)
     if not isinstance(d, dict):
         raise ValueError("json: cannot unmarshal non-object into Go value of type bitcoin.Message")
     t = int(_field(d, "Type", lambda v: isinstance(v, _IntLit) and -(1 << 63) <= v < 1 << 63, 0))

@@ -33,7 +33,8 @@ def run(hostport: str, engine=None, params=None, on_client=None) -> int:
     `on_client` (tests) receives the LSP client once connected."""
     try:
         c = lsp.NewClient(hostport, params or params_from_env())
-    except lsp.LSPError:
+    except lsp.LSPError as e:
+        _log(str(e))
         return 1
     if on_client is not None:
         on_client(c)
@@ -76,7 +77,8 @@ def run(hostport: str, engine=None, params=None, on_client=None) -> int:
                 raise
             c.Write(marshal(NewResult(h, n)))
             jobs += 1
-    except lsp.LSPError:
+    except lsp.LSPError as e:
+        _log(f"server lost after {jobs} job(s): {e}")
         return 0  # server lost: shut down (p1.pdf p.15)
     finally:
         c.Close()

@@ -359,8 +359,8 @@ def serve(port: int, params=None, job_size: int | None = None, ready=None, log=N
             if e.conn_id == 0:
                 return  # server closed
             note = sched.lost(e.conn_id)
-            if log and note:
-                log(note)
+            if log:  # the LSP's reason (silent epochs, last heard) beside what it cost
+                log(f"{e}: {note}" if note else str(e))
             dispatch()
             continue
         try:

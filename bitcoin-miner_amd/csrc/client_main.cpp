@@ -22,6 +22,12 @@ void printResult(uint64_t hash, uint64_t nonce) {  // client.go:19-21
 
 void printDisconnected() { std::printf("Disconnected\n"); }  // client.go:24-26
 
+// why, on stderr (stdout is graded, p1.pdf p.15)
+void why_disconnected(lspn::Client& c) {
+    const std::string r = c.lost_reason();
+    std::fprintf(stderr, "client: connection lost%s%s%s\n", r.empty() ? "" : " (", r.c_str(), r.empty() ? "" : ")");
+}
+
 bool parse_uint(const std::string& s, uint64_t& out) {  // strconv.ParseUint(s, 10, 64)
     if (s.empty() || s.size() > 20) return false;
     unsigned __int128 v = 0;
@@ -49,6 +55,7 @@ int main(int argc, char** argv) {
     lspn::Params params;
     lspn::Client client(params);
     if (!client.connect(argv[1])) {
+        why_disconnected(client);
         printDisconnected();
         return 0;
     }
@@ -58,6 +65,7 @@ int main(int argc, char** argv) {
     req.lower = 0;
     req.upper = max_nonce;
     if (!client.write(lspn::btc_marshal(req))) {
+        why_disconnected(client);
         printDisconnected();
         return 0;
     }
@@ -70,6 +78,7 @@ int main(int argc, char** argv) {
         client.close();
         return 0;
     }
+    why_disconnected(client);
     printDisconnected();
     return 0;
 }

@@ -54,6 +54,8 @@ struct Dev {
     unsigned long long* h_clk = nullptr;
     size_t clk_cap = 0;  // groups
     std::vector<hipEvent_t> ev;
+    hipEvent_t done = nullptr;  // blocking-sync event: the end of a call's work (host_wait)
+    int wait_mode = 0;          // HostWait
     // per-call results
     int rc = GPUHASH_OK;
     uint64_t best_h = ~0ull, best_n = ~0ull;
@@ -96,6 +98,45 @@ struct DeviceGuard {
         if ((expr) != hipSuccess) return GPUHASH_EHIP; \
     } while (0)
 
+// How the host waits for a call's work (GPUHASH_HOST_WAIT, read at gpuhash_open):
+//   poll    (default) hipEventQuery on a completion event: back to back for the first
+//           0.5 ms (short calls return at once), then every 100 us with the thread asleep
+//   stream  hipStreamSynchronize on the device's stream
+//   event   hipEventSynchronize on the event, created with hipEventBlockingSync
+// A miner spends almost all its life inside this wait (a 2^34-nonce job is ~0.5 s of GPU
+// time, ~4 s with 8 miners on one GPU).  On this ROCm both `stream` and `event` keep the
+// waiting thread running: 8 miners sharing one MI355X burned 1.0 host core each (8 of the
+// box's 16-CPU quota), `poll` 0.007 core each, at the same GPU throughput and the same
+// bench GH/s (tools/host_wait_probe.py, profiles/r05_host_wait.jsonl).
+enum HostWait { kWaitPoll = 0, kWaitStream = 1, kWaitEvent = 2 };
+
+static int host_wait_mode() {
+    const char* e = std::getenv("GPUHASH_HOST_WAIT");
+    if (e && !std::strcmp(e, "stream")) return kWaitStream;
+    if (e && !std::strcmp(e, "event")) return kWaitEvent;
+    return kWaitPoll;
+}
+
+static int host_wait(Dev& d) {
+    if (d.wait_mode == kWaitStream) {
+        HIPCHK(hipStreamSynchronize(d.stream));
+        return GPUHASH_OK;
+    }
+    HIPCHK(hipEventRecord(d.done, d.stream));
+    if (d.wait_mode == kWaitEvent) {
+        HIPCHK(hipEventSynchronize(d.done));
+        return GPUHASH_OK;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipEventQuery(d.done);
+        if (q == hipSuccess) return GPUHASH_OK;
+        if (q != hipErrorNotReady) return GPUHASH_EHIP;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(500))
+            std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+}
+
 static int dev_init(Dev& d, int ord, int shard) {
     d.ord = ord;
     d.shard = shard;
@@ -106,6 +147,8 @@ static int dev_init(Dev& d, int ord, int shard) {
     HIPCHK(hipStreamGetDevice(d.stream, &sd));
     if (sd != ord) return GPUHASH_EHIP;  // the stream must live on the device it serves
     d.stream_dev = sd;
+    d.wait_mode = host_wait_mode();
+    HIPCHK(hipEventCreateWithFlags(&d.done, hipEventBlockingSync | hipEventDisableTiming));
     if (hipMalloc(&d.d_thresh, sizeof(unsigned long long)) != hipSuccess) return GPUHASH_ENOMEM;
     if (hipMalloc(&d.d_ncand, sizeof(unsigned int)) != hipSuccess) return GPUHASH_ENOMEM;
     if (hipMalloc(&d.d_best, sizeof(Cand)) != hipSuccess) return GPUHASH_ENOMEM;
@@ -121,6 +164,7 @@ static void dev_free(Dev& d) {
     if (d.stream) hipStreamSynchronize(d.stream);
     for (auto e : d.ev) hipEventDestroy(e);
     d.ev.clear();
+    if (d.done) hipEventDestroy(d.done);
     if (d.d_thresh) hipFree(d.d_thresh);
     if (d.d_ncand) hipFree(d.d_ncand);
     if (d.d_best) hipFree(d.d_best);
@@ -327,7 +371,7 @@ static int dev_run(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t
     if (mode == 0) HIPCHK(launch_reduce(d.d_cands, d.d_ncand, d.d_best, d.stream));
     HIPCHK(hipMemcpyAsync(d.h_best, d.d_best, sizeof(Cand), hipMemcpyDeviceToHost, d.stream));
     HIPCHK(hipMemcpyAsync(d.h_clk, d.d_meta, kCounterBytes * groups.size(), hipMemcpyDeviceToHost, d.stream));
-    HIPCHK(hipStreamSynchronize(d.stream));
+    if ((rc = host_wait(d))) return rc;
     for (size_t g = 0; g < groups.size(); g++) {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, d.ev[2 * g], d.ev[2 * g + 1]));

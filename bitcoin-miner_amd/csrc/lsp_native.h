@@ -15,6 +15,9 @@
 //     machine as bitcoin-miner_amd/lsp/endpoint.py; client_api.go / server_api.go shape
 //     the APIs.  One background thread per endpoint owns the socket and the epochs, so
 //     heartbeats continue while the program's main thread blocks in a long search.
+//   * diagnostics: a lost connection carries its reason (silent epochs, when the peer was
+//     last heard), and the event loop records how late its epochs fire; LSP_DIAG=1 prints
+//     every epoch that fires more than one epoch late to stderr (as lsp/endpoint.py).
 #pragma once
 
 #include <arpa/inet.h>
@@ -27,6 +30,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -419,8 +423,13 @@ inline std::string b64encode(const std::string& in) {
     return out;
 }
 
-inline bool b64decode(const std::string& in, std::string& out) {
+// base64.StdEncoding.Decode: padded standard alphabet; '\r' and '\n' are ignored
+inline bool b64decode(const std::string& raw, std::string& out) {
     const char* A = b64_alphabet();
+    std::string in;
+    in.reserve(raw.size());
+    for (char c : raw)
+        if (c != '\r' && c != '\n') in += c;
     if (in.size() % 4) return false;
     out.clear();
     for (size_t i = 0; i < in.size(); i += 4) {
@@ -464,10 +473,15 @@ inline bool lsp_unmarshal(const std::string& raw, LspMsg& m) {
     if (!JsonReader(raw).object(o)) return false;
     if (!get_int(o, "Type", m.type) || !get_int(o, "ConnID", m.conn) || !get_int(o, "SeqNum", m.seq)) return false;
     // []byte: each string member is base64-decoded in order (an invalid one fails the
-    // message), null leaves the previous value
+    // message); null sets a slice back to nil, as encoding/json does
     m.has_payload = false;
+    m.payload.clear();
     return jfields(o, "Payload", [&](const JVal& f) {
-        if (f.kind == JVal::Null) return true;
+        if (f.kind == JVal::Null) {
+            m.has_payload = false;
+            m.payload.clear();
+            return true;
+        }
         if (f.kind != JVal::Str || !b64decode(f.text, m.payload)) return false;
         m.has_payload = true;
         return true;
@@ -623,9 +637,13 @@ class Conn {
         pump();
     }
 
+    // why the connection was lost ("" while it is not)
+    const std::string& lost_reason() const { return lost_reason_; }
+
     // a message from the peer; payloads that became deliverable in order go to `out`
     void on_message(const LspMsg& m, std::deque<std::string>& out) {
         silent_ = 0;
+        last_heard_ = std::chrono::steady_clock::now();
         if (m.type == MsgAck) {
             if (unacked_.erase(m.seq)) pump();
             return;
@@ -650,6 +668,10 @@ class Conn {
         if (lost_) return false;
         if (++silent_ >= k_) {
             lost_ = true;
+            const auto ago = std::chrono::duration_cast<std::chrono::milliseconds>(
+                std::chrono::steady_clock::now() - last_heard_).count();
+            lost_reason_ = std::to_string(silent_) + " silent epochs, peer last heard " + std::to_string(ago) +
+                           " ms ago";
             return true;
         }
         if (!got_data_) send_(LspMsg{MsgAck, id_, 0, false, {}});
@@ -657,7 +679,10 @@ class Conn {
         for (long long seq : recent_) send_(LspMsg{MsgAck, id_, seq, false, {}});
         return false;
     }
-    void heard() { silent_ = 0; }
+    void heard() {
+        silent_ = 0;
+        last_heard_ = std::chrono::steady_clock::now();
+    }
 
    private:
     long long id_;
@@ -665,6 +690,8 @@ class Conn {
     std::function<void(const LspMsg&)> send_;
     bool lost_ = false, got_data_ = false;
     int silent_ = 0;
+    std::chrono::steady_clock::time_point last_heard_ = std::chrono::steady_clock::now();
+    std::string lost_reason_;
     long long next_seq_ = 1, expected_ = 1;
     std::deque<std::pair<long long, std::string>> pending_;  // not yet inside the window
     std::map<long long, std::string> unacked_;               // sent, not acknowledged
@@ -687,13 +714,24 @@ class Conn {
     }
 };
 
+// How late the event loop's epochs fire (written under the endpoint's mutex).
+struct LoopLateness {
+    long long max_ms = 0;  // the latest any epoch fired after it was due
+    long long late_epochs = 0;  // epochs that fired more than one epoch late
+};
+
 // Runs `tick(now_is_epoch)` under `mu` whenever the socket is readable, at least every
 // 50 ms, until `stop` is set: the event loop both endpoints share.
 template <class Tick>
-void event_loop(int fd, int epoch_ms, std::mutex& mu, const bool& stop, Tick&& tick) {
+void event_loop(int fd, int epoch_ms, std::mutex& mu, const bool& stop, LoopLateness& late, const char* role,
+                Tick&& tick) {
     using clk = std::chrono::steady_clock;
     const auto epoch = std::chrono::milliseconds(std::max(1, epoch_ms));
+    const char* d = std::getenv("LSP_DIAG");
+    const bool diag = d && *d && std::strcmp(d, "0") != 0;
     auto next = clk::now() + epoch;
+    auto win_start = clk::now();
+    long long win_max = 0;
     for (;;) {
         {
             std::lock_guard<std::mutex> lk(mu);
@@ -704,8 +742,28 @@ void event_loop(int fd, int epoch_ms, std::mutex& mu, const bool& stop, Tick&& t
         pollfd pfd{fd, POLLIN, 0};
         poll(&pfd, 1, std::min(timeout, 50));
         std::lock_guard<std::mutex> lk(mu);
-        bool is_epoch = clk::now() >= next;
-        if (is_epoch) next = clk::now() + epoch;
+        const auto t = clk::now();
+        bool is_epoch = t >= next;
+        if (is_epoch) {
+            const long long ms = std::chrono::duration_cast<std::chrono::milliseconds>(t - next).count();
+            late.max_ms = std::max(late.max_ms, ms);
+            if (ms > epoch.count()) {
+                late.late_epochs++;
+                if (diag)
+                    std::fprintf(stderr, "%s[%d]: epoch fired %lld ms late (epoch %lld ms)\n", role, (int)getpid(), ms,
+                                 (long long)epoch.count());
+            }
+            if (diag) {  // every 5 s: the latest epoch of the window
+                win_max = std::max(win_max, ms);
+                if (t - win_start >= std::chrono::seconds(5)) {
+                    std::fprintf(stderr, "%s[%d]: window max lateness %lld ms, run max %lld ms, %lld epochs >1 late\n",
+                                 role, (int)getpid(), win_max, late.max_ms, late.late_epochs);
+                    win_max = 0;
+                    win_start = t;
+                }
+            }
+            next = t + epoch;
+        }
         tick(is_epoch);
     }
 }
@@ -722,10 +780,21 @@ class Client {
     bool connect(const std::string& hostport) {
         if (!udp_.dial(hostport)) return false;
         udp_.write(lsp_marshal(LspMsg{MsgConnect, 0, 0, false, {}}), udp_.peer());
-        thread_ = std::thread([this] { event_loop(udp_.fd(), p_.epoch_ms, mu_, stop_, [this](bool e) { tick(e); }); });
+        thread_ = std::thread([this] {
+            event_loop(udp_.fd(), p_.epoch_ms, mu_, stop_, late_, "lsp-client", [this](bool e) { tick(e); });
+        });
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [this] { return conn_ || failed_; });
         return conn_ != nullptr;
+    }
+
+    // Why the connection failed or was lost, with this loop's latest epoch ("" if it was not).
+    std::string lost_reason() {
+        std::lock_guard<std::mutex> lk(mu_);
+        std::string r = failed_ ? "no connect ack in " + std::to_string(connect_silent_) + " epochs"
+                                : (conn_ && conn_->lost() ? conn_->lost_reason() : std::string());
+        if (!r.empty()) r += "; this loop's latest epoch " + std::to_string(late_.max_ms) + " ms late";
+        return r;
     }
 
     // Next in-order payload; false once the connection is lost and nothing is queued.
@@ -762,6 +831,7 @@ class Client {
     std::condition_variable cv_;
     bool stop_ = false, failed_ = false;
     int connect_silent_ = 0;
+    LoopLateness late_;
     std::unique_ptr<Conn> conn_;
     std::deque<std::string> reads_;
 
@@ -816,6 +886,7 @@ class Server {
         long long conn = 0;
         bool lost = false;  // the connection was lost (or closed); no payload
         std::string payload;
+        std::string reason;  // for `lost`: why ("closed" for a flushed close)
     };
 
     explicit Server(const Params& p) : p_(p), udp_(true) {}
@@ -823,7 +894,9 @@ class Server {
 
     bool listen(int port) {
         if (!udp_.listen(port)) return false;
-        thread_ = std::thread([this] { event_loop(udp_.fd(), p_.epoch_ms, mu_, stop_, [this](bool e) { tick(e); }); });
+        thread_ = std::thread([this] {
+            event_loop(udp_.fd(), p_.epoch_ms, mu_, stop_, late_, "lsp-server", [this](bool e) { tick(e); });
+        });
         return true;
     }
     int port() const { return udp_.port(); }
@@ -864,6 +937,7 @@ class Server {
     std::map<long long, Addr> addr_of_;
     std::map<long long, std::unique_ptr<Conn>> conns_;
     std::deque<Event> events_;
+    LoopLateness late_;
 
     void stop() {
         {
@@ -874,6 +948,10 @@ class Server {
     }
 
     void drop(long long id, bool notify) {  // mu_ held
+        std::string why = "closed";
+        auto c = conns_.find(id);
+        if (c != conns_.end() && c->second->lost())
+            why = c->second->lost_reason() + "; this loop's latest epoch " + std::to_string(late_.max_ms) + " ms late";
         auto a = addr_of_.find(id);
         if (a != addr_of_.end()) {
             id_of_.erase(a->second);
@@ -881,7 +959,7 @@ class Server {
         }
         conns_.erase(id);
         if (notify) {
-            events_.push_back(Event{id, true, {}});
+            events_.push_back(Event{id, true, {}, why});
             cv_.notify_all();
         }
     }
@@ -915,7 +993,7 @@ class Server {
             if (c == conns_.end() || addr_of_[m.conn] != from) continue;
             got.clear();
             c->second->on_message(m, got);
-            for (auto& p : got) events_.push_back(Event{m.conn, false, std::move(p)});
+            for (auto& p : got) events_.push_back(Event{m.conn, false, std::move(p), {}});
             if (!got.empty()) cv_.notify_all();
         }
         if (is_epoch) {

@@ -80,7 +80,7 @@ int main(int argc, char** argv) {
     lspn::Params params;
     lspn::Client client(params);
     if (!client.connect(argv[1])) {
-        logf("could not connect to %s", argv[1]);
+        logf("could not connect to %s (%s)", argv[1], client.lost_reason().c_str());
         return 1;
     }
     std::vector<int> devs = devices_from_env();
@@ -91,6 +91,7 @@ int main(int argc, char** argv) {
         return 1;
     }
     int status = 0;
+    long long jobs = 0;
     if (client.write(lspn::btc_marshal(BtcMsg{}))) {  // json.Marshal(bitcoin.NewJoin())
         std::string payload;
         while (client.read(payload)) {
@@ -123,8 +124,11 @@ int main(int argc, char** argv) {
                 break;
             }
             if (!client.write(result_json(h, n))) break;
+            jobs++;
         }
     }
+    const std::string why = client.lost_reason();
+    if (!why.empty()) logf("server lost after %lld job(s): %s", jobs, why.c_str());
     gpuhash_close(ctx);
     if (status == 0) client.close();  // flush the last Result; the server is gone otherwise
     return status;

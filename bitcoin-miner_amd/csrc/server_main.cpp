@@ -283,6 +283,7 @@ int main(int argc, char** argv) {
     for (;;) {
         lspn::Server::Event e = srv.read();
         if (e.lost) {
+            logf("connection %lld %s", e.conn, e.reason == "closed" ? "closed" : ("lost (" + e.reason + ")").c_str());
             sched.lost(e.conn);
             dispatch();
             continue;

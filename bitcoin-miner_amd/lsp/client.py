@@ -30,14 +30,15 @@ class Client:
         self._failed = False
         self._closed = False
         self._connect_silent = 0
+        self.lost_reason = ""
         self._loop = Loop(self._conn, self._p.EpochMillis, self._on_datagram, self._on_command,
-                          self._on_epoch)
+                          self._on_epoch, role="lsp-client")
         self._loop.start()
         self._send(NewConnect())
         self._connected.wait()
         if self._failed:
             self._shutdown()
-            raise LSPError(f"could not connect to {hostport}")
+            raise LSPError(f"could not connect to {hostport} ({self.lost_reason})")
 
     # ---- API -----------------------------------------------------------------
     def ConnID(self) -> int:
@@ -102,6 +103,7 @@ class Client:
             self._connect_silent += 1
             if self._connect_silent >= self._p.EpochLimit:
                 self._failed = True
+                self.lost_reason = f"no connect ack in {self._connect_silent} epochs"
                 self._connected.set()
             else:
                 self._send(NewConnect())
@@ -109,7 +111,9 @@ class Client:
         was_lost = self._st.lost
         self._st.on_epoch()
         if self._st.lost and not was_lost:
-            self._reads.put(("err", "connection lost"))
+            self.lost_reason = (f"{self._st.lost_reason}; this loop's latest epoch "
+                                f"{1000 * self._loop.max_late:.0f} ms late")
+            self._reads.put(("err", f"connection lost ({self.lost_reason})"))
         self._check_close()
 
     def _check_close(self) -> None:

@@ -12,13 +12,21 @@ lsp/server_impl.go, which cannot carry data as written -- SURVEY.md 2 rows 8-9):
 
 Like the reference's design (one handleMessages goroutine per endpoint), one loop
 thread owns all protocol state; API calls post commands to it through a queue.
+
+Diagnostics: a lost connection carries its reason -- the silent
+epochs and how long ago the peer was last heard -- and the loop records how late its
+epochs fire (`max_late`: a loop thread that is not scheduled, or waits for the GIL, stops
+heartbeating its peers).  LSP_DIAG=1 prints every epoch that fires more than one epoch
+late to stderr as it happens, and every 5 s the latest lateness of that window.
 """
 from __future__ import annotations
 
 import collections
+import os
 import queue
 import selectors
 import socket
+import sys
 import threading
 import time
 
@@ -42,6 +50,8 @@ class ConnState:
         self.got_data = False
         self.silent = 0
         self.lost = False
+        self.lost_reason = ""
+        self.last_heard = time.monotonic()
         self.closing = False
 
     # -- sending ---------------------------------------------------------------
@@ -71,6 +81,7 @@ class ConnState:
     def on_message(self, m: Message) -> list:
         """Handles one message from the peer; returns payloads now deliverable in order."""
         self.silent = 0
+        self.last_heard = time.monotonic()
         if m.Type == MsgType.MsgAck:
             if m.SeqNum in self.unacked:
                 del self.unacked[m.SeqNum]
@@ -97,6 +108,8 @@ class ConnState:
         self.silent += 1
         if self.silent >= self.k:
             self.lost = True
+            self.lost_reason = (f"{self.silent} silent epochs, peer last heard "
+                                f"{1000 * (time.monotonic() - self.last_heard):.0f} ms ago")
             return
         if not self.got_data:
             self.send(NewAck(self.conn_id, 0))
@@ -109,9 +122,15 @@ class ConnState:
 class Loop:
     """Event loop thread: UDP readiness, a command queue with a wakeup socket, epochs."""
 
-    def __init__(self, conn, epoch_ms: int, on_datagram, on_command, on_epoch):
+    def __init__(self, conn, epoch_ms: int, on_datagram, on_command, on_epoch, role: str = "lsp"):
         self.conn = conn
         self.epoch = epoch_ms / 1000.0
+        self.role = role
+        self.max_late = 0.0   # seconds: the latest any epoch fired after it was due
+        self.late_epochs = 0  # epochs that fired more than one epoch late
+        self._diag = os.environ.get("LSP_DIAG", "") not in ("", "0")
+        self._win_late = 0.0                  # LSP_DIAG: latest epoch of the current 5-s window
+        self._win_start = time.monotonic()
         self.on_datagram, self.on_command, self.on_epoch = on_datagram, on_command, on_epoch
         self.cmds = queue.Queue()
         self._r, self._w = socket.socketpair()
@@ -164,8 +183,24 @@ class Loop:
                     except queue.Empty:
                         break
                     self.on_command(cmd)
-                if time.monotonic() >= next_epoch:
-                    next_epoch = time.monotonic() + self.epoch
+                now = time.monotonic()
+                if now >= next_epoch:
+                    late = now - next_epoch
+                    if late > self.max_late:
+                        self.max_late = late
+                    if late > self.epoch:
+                        self.late_epochs += 1
+                        if self._diag:
+                            print(f"{self.role}[{os.getpid()}]: epoch fired {1000 * late:.0f} ms late "
+                                  f"(epoch {1000 * self.epoch:.0f} ms)", file=sys.stderr, flush=True)
+                    if self._diag:
+                        self._win_late = max(self._win_late, late)
+                        if now - self._win_start >= 5.0:
+                            print(f"{self.role}[{os.getpid()}]: window max lateness {1000 * self._win_late:.1f} ms, "
+                                  f"run max {1000 * self.max_late:.1f} ms, {self.late_epochs} epochs >1 late",
+                                  file=sys.stderr, flush=True)
+                            self._win_late, self._win_start = 0.0, now
+                    next_epoch = now + self.epoch
                     self.on_epoch()
         finally:
             sel.close()

@@ -8,9 +8,24 @@ with the reference's Go programs.
 from __future__ import annotations
 
 import base64
+import binascii
 import enum
 import json
 from dataclasses import dataclass
+
+import gojson
+
+
+def b64decode_go(s: str) -> bytes:
+    """base64.StdEncoding.DecodeString as encoding/json applies it to a []byte: padded
+    standard alphabet, '\\r' and '\\n' ignored, anything else malformed -> ValueError."""
+    t = s.replace("\r", "").replace("\n", "")
+    if len(t) % 4:
+        raise ValueError("illegal base64 data: length")
+    try:
+        return base64.b64decode(t.encode("ascii"), validate=True)
+    except (binascii.Error, UnicodeEncodeError) as e:
+        raise ValueError(f"illegal base64 data: {e}") from None
 
 
 class MsgType(enum.IntEnum):
@@ -33,16 +48,29 @@ class Message:
 
     @staticmethod
     def unmarshal(raw: bytes) -> "Message":
-        # encoding/json field matching: keys ignore (ASCII) case, the last one wins, unknown
-        # keys of any shape are skipped (as csrc/lsp_native.h)
-        d = json.loads(raw, object_pairs_hook=lambda pairs: {k.lower(): v for k, v in pairs
-                                                             if k.isascii()})
-        p = d.get("payload")
-        return Message(MsgType(int(d["type"])), int(d.get("connid", 0)), int(d.get("seqnum", 0)),
-                       None if p is None else base64.b64decode(p))
+        """json.Unmarshal into lsp.Message, with the same Go rules as bitcoin.unmarshal and
+        csrc/lsp_native.h lsp_unmarshal (gojson): keys match ignoring (ASCII) case, every
+        matching member decodes in order, a wrong-typed member fails the message (ValueError),
+        an absent field keeps its zero value (Type 0 = MsgConnect).  Type / ConnID / SeqNum
+        are ints (integer literals only); Payload is a []byte: a string member is base64
+        (StdEncoding, padded, CR / LF ignored), and null resets it to nil.  A Type outside
+        the three kinds is kept as a plain int (the endpoints then ignore the message)."""
+        d = gojson.loads(raw)
+        if not isinstance(d, dict):
+            raise ValueError("json: cannot unmarshal non-object into Go value of type lsp.Message")
+        t, conn, seq = gojson.i64(d, "Type"), gojson.i64(d, "ConnID"), gojson.i64(d, "SeqNum")
+        payload = None
+        for v in d.get("payload", ()):
+            if v is None:
+                payload = None
+            elif isinstance(v, str):
+                payload = b64decode_go(v)
+            else:
+                raise ValueError(f"json: cannot unmarshal {v!r} into Go struct field Message.Payload")
+        return Message(MsgType(t) if t in MsgType._value2member_map_ else t, conn, seq, payload)
 
     def __str__(self) -> str:  # message.go String()
-        name = {MsgType.MsgConnect: "Connect", MsgType.MsgData: "Data", MsgType.MsgAck: "Ack"}[self.Type]
+        name = {MsgType.MsgConnect: "Connect", MsgType.MsgData: "Data", MsgType.MsgAck: "Ack"}.get(self.Type, "Unknown")
         payload = " " + (self.Payload or b"").decode(errors="replace") if self.Type == MsgType.MsgData else ""
         return f"[{name} {self.ConnID} {self.SeqNum}{payload}]"
 

@@ -32,7 +32,7 @@ class Server:
         self._closed = False
         self._lost_during_close = False
         self._loop = Loop(self._conn, self._p.EpochMillis, self._on_datagram, self._on_command,
-                          self._on_epoch)
+                          self._on_epoch, role="lsp-server")
         self._loop.start()
 
     # ---- API -----------------------------------------------------------------
@@ -133,7 +133,8 @@ class Server:
                 if self._closing_all:
                     self._lost_during_close = True
                 self._drop(cid)
-                self._reads.put(("err", cid, f"connection {cid} lost"))
+                self._reads.put(("err", cid, f"connection {cid} lost ({st.lost_reason}; this loop's "
+                                             f"latest epoch {1000 * self._loop.max_late:.0f} ms late)"))
             elif st.closing and st.flushed():
                 self._drop(cid)
                 if not self._closing_all:

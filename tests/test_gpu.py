@@ -572,3 +572,19 @@ def test_concurrent_calls_on_one_context_are_serialised(engine, oracle):
     for t in ts:
         t.join(60)
     assert got == [oracle.min(*j) for j in jobs]
+
+
+def test_host_wait_does_not_spin(engine):
+    """A miner spends its life waiting inside gpuhash_min.  On this ROCm both
+    hipStreamSynchronize and a blocking-sync event keep the waiting thread running (1.0
+    host core per miner, profiles/r05_host_wait.jsonl); the engine's default wait sleeps
+    between event queries, so a 0.5-s search costs the host almost nothing."""
+    import resource
+    import time
+    engine.min(b"bradfitz", 0, 1 << 20)
+    r0, t0 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter()
+    engine.min(b"bradfitz", 1 << 36, (1 << 36) + (1 << 34) - 1)
+    wall = time.perf_counter() - t0
+    r1 = resource.getrusage(resource.RUSAGE_SELF)
+    cpu = (r1.ru_utime - r0.ru_utime) + (r1.ru_stime - r0.ru_stime)
+    assert wall > 0.2 and cpu / wall < 0.15, (cpu, wall)

@@ -4,8 +4,9 @@ LSP/UDP on localhost (BASELINE configs 1 and 5, reduced in size for a 1-GPU box)
 Config 1: `server` + one miner + `client host:port bradfitz 9999` must print exactly
 "Result 1419516646206828 9898" (p1.pdf p.15 output format).
 Config 5 at full size (test_config5_full_size): 16 clients x [0, 2^36], 8 miners sharing
-the GPU, 10% drops on every role, a SIGKILLed miner; four clients checked against CPU
-goldens (oracle/golden_scan.c), the rest against a direct search + oracle re-hash.
+the GPU, 10% drops on every role, a SIGKILLed miner; all sixteen clients checked against
+their CPU goldens (oracle/golden_scan.c) and re-hashed by the oracle, with LSP and cgroup
+diagnostics recorded (tests/sysdiag.py).
 Config 5 (scaled): 8 clients, 4 miners sharing the GPU, lspnet read and write drops of
 10% on every role, and one miner SIGKILLed mid-job.  Every client's printed result must
 equal a direct search of its whole range, and the winner must re-hash (oracle) to the
@@ -21,6 +22,7 @@ import time
 import pytest
 
 pytestmark = pytest.mark.gpu
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "bitcoin-miner_amd", "bin")
@@ -211,16 +213,20 @@ def test_config5_full_size(procs, engine, oracle, golden):
     one miner SIGKILLed mid-job, whose job must be re-run.  Every client is checked against
     its CPU golden (tests/golden/make_golden.py --huge: the SHA-NI / AVX-512 restatement
     over the whole [0, 2^36], all 16 since round 4), and every printed winner is re-hashed
-    by the oracle."""
+    by the oracle.
+
+    200 ms epochs, 10 of them before a connection counts as lost (2 s), as in the other
+    system tests.  Every program runs with LSP_DIAG=1, so a lost connection says why (its
+    silent epochs, when the peer was last heard) and each LSP loop reports how late its
+    epochs fired; the cgroup's CPU use and CFS throttling are sampled throughout, and the
+    miners' CPU time is read before they are stopped.  All of it goes to
+    $GPUHASH_DIAG_DIR/config5_diag.json and into the failure message."""
     import time as _t
+    import sysdiag
     gold = {r["name"]: r for r in golden["ranges"]}
     port = free_port()
     drops = dict(LSPNET_CLIENT_READ_DROP=10, LSPNET_CLIENT_WRITE_DROP=10,
-                 LSPNET_SERVER_READ_DROP=10, LSPNET_SERVER_WRITE_DROP=10)
-    # 200 ms epochs as in the other tests, but 25 of them (5 s, still half the reference's
-    # default 2 s x 5) before a connection counts as lost: 25 processes share the box's CPU
-    # share here, and one round-4 run lost a client after 2 s (10 epochs) of silence
-    drops = dict(drops, LSP_EPOCH_LIMIT=25)
+                 LSPNET_SERVER_READ_DROP=10, LSPNET_SERVER_WRITE_DROP=10, LSP_DIAG=1)
     server = procs.start([os.path.join(BIN, "server"), str(port)], env=env(GPUHASH_SERVER_LOG=1, **drops))
     time.sleep(0.5)
     miners = [procs.start([os.path.join(BIN, "miner"), f"127.0.0.1:{port}"], env=env(**drops))
@@ -228,18 +234,44 @@ def test_config5_full_size(procs, engine, oracle, golden):
     miners += [start_native(procs, port, **drops) for _ in range(4)]
     time.sleep(4.0)  # let the miners open the GPU and join
     max_nonce = 1 << 36
+    sampler = sysdiag.CgroupSampler()
+    sampler.start()
+    cpu0 = {m.pid: sysdiag.proc_cpu(m.pid) for m in miners}
     t0 = _t.time()
     clients = [procs.start([os.path.join(BIN, "client"), f"127.0.0.1:{port}", f"client-{i:02d}",
                             str(max_nonce)], env=env(**drops)) for i in range(16)]
     time.sleep(3.0)
     miners[1].send_signal(signal.SIGKILL)  # mid-job (2^34-nonce jobs take ~4 s per miner here)
-    outs = [c.communicate(timeout=400)[0].strip() for c in clients]
+    res = [c.communicate(timeout=400) for c in clients]
     wall = _t.time() - t0
-    if any(not o.startswith("Result") for o in outs):  # show the server's account of it
-        server.send_signal(signal.SIGTERM)
-        log = server.communicate(timeout=30)[1]
-        raise AssertionError(f"clients {[i for i, o in enumerate(outs) if not o.startswith('Result')]} "
-                             f"did not get a Result; server log tail:\n{log[-4000:]}")
+    cpu1 = {m.pid: sysdiag.proc_cpu(m.pid) for m in miners}
+    cgroup = sampler.stop()
+    outs = [o.strip() for o, _ in res]
+    server.send_signal(signal.SIGTERM)
+    log = server.communicate(timeout=30)[1]
+    for m in miners:
+        if m.poll() is None:
+            m.send_signal(signal.SIGTERM)
+    merr = [m.communicate(timeout=30)[1] for m in miners]
+    miner_cpu = [None if cpu0[m.pid] is None or cpu1[m.pid] is None else round(cpu1[m.pid] - cpu0[m.pid], 2)
+                 for m in miners]
+    texts = {"server": log, **{f"client-{i:02d}": e for i, (_, e) in enumerate(res)},
+             **{f"miner-{k}": e for k, e in enumerate(merr)}}
+    late = sysdiag.lsp_lateness(texts)
+    failed = [i for i, o in enumerate(outs) if not o.startswith("Result")]
+    diag = {"wall_s": round(wall, 2), "failed_clients": failed,
+            "failed_client_stderr": {i: res[i][1][-1500:] for i in failed},
+            "cgroup": cgroup,
+            "miner_cpu_s": miner_cpu, "miner_cpu_per_wall": [None if c is None else round(c / wall, 3)
+                                                               for c in miner_cpu],
+            "max_late_ms": {k: v["max_late_ms"] for k, v in late.items()},
+            "late_epochs": {k: v["late_epochs"] for k, v in late.items() if v["late_epochs"]},
+            "server_losses": [ln for ln in log.splitlines() if " lost" in ln or "abandoned" in ln]}
+    sysdiag.write_diag("config5_diag.json", diag)
+    print("config 5 diagnostics:", diag)
+    if failed:  # show the LSP's account of it
+        raise AssertionError(f"clients {failed} did not get a Result; diagnostics {diag}; "
+                             f"server log tail:\n{log[-4000:]}")
     checked_golden = 0
     for i, out in enumerate(outs):
         parts = out.split()
@@ -252,7 +284,5 @@ def test_config5_full_size(procs, engine, oracle, golden):
         checked_golden += 1
         assert oracle.hash(msg, n) == h
     assert checked_golden == 16
-    server.send_signal(signal.SIGTERM)
-    log = server.communicate(timeout=30)[1]
     assert "lost; job [" in log and "requeued" in log, log[-2000:]
     print(f"config 5 full size: 16 x 2^36 nonces in {wall:.1f} s = {16 * (max_nonce + 1) / wall / 1e9:.1f} GH/s")

@@ -2,7 +2,10 @@
 csrc/lsp_native.h btc_unmarshal (compiled server/miner) -- decode every document of a
 corpus the way Go's json.Unmarshal into bitcoin.Message (message.go:16-21) does, and so
 agree with each other byte for byte (invalid UTF-8 one U+FFFD per byte,
-malformed nested values rejected, duplicate keys with null / wrong-type members)."""
+malformed nested values rejected, duplicate keys with null / wrong-type members).  The
+same for the LSP frame readers, lsp.Message.unmarshal and lsp_native.h lsp_unmarshal, on
+lsp.Message (lsp/message.go:17-22): []byte Payload null resets it to nil, int fields take
+integer literals only."""
 import os
 import subprocess
 
@@ -117,3 +120,97 @@ def test_readers_agree_on_random_byte_strings(probe):
         raw = raw.replace(b'"', b"'").replace(b"\\", b"/")
         docs.append(b'{"Type":1,"Data":"' + raw + b'","Lower":0,"Upper":7}')
     assert _native(probe, docs) == [_python(d) for d in docs]
+
+
+# (frame, expected) for lsp.Message -- None: Go's Unmarshal errors; else
+# (Type, ConnID, SeqNum, Payload bytes or None for nil)
+LSP_CASES = [
+    (b'{"Type":1,"ConnID":3,"SeqNum":4,"Payload":"aGk="}', (1, 3, 4, b"hi")),
+    (b'{"Type":2,"ConnID":3,"SeqNum":4,"Payload":null}', (2, 3, 4, None)),
+    (b'{"Type":1,"ConnID":3,"SeqNum":4}', (1, 3, 4, None)),
+    # []byte: a later null resets the slice to nil (ADVICE r04 on lsp_native.h)
+    (b'{"Type":1,"ConnID":3,"SeqNum":4,"Payload":"aGk=","payload":null}', (1, 3, 4, None)),
+    (b'{"Type":1,"ConnID":3,"SeqNum":4,"payload":null,"PAYLOAD":"aGk="}', (1, 3, 4, b"hi")),
+    (b'{"Type":1,"Payload":"aGk=","payload":"eW8="}', (1, 0, 0, b"yo")),
+    # base64: StdEncoding, padded; CR/LF ignored; other junk fails the frame
+    (b'{"Type":1,"Payload":"aG\\r\\nk="}', (1, 0, 0, b"hi")),
+    (b'{"Type":1,"Payload":"aGk"}', None),
+    (b'{"Type":1,"Payload":"a$Gk="}', None),
+    (b'{"Type":1,"Payload":5}', None),
+    (b'{"Type":1,"Payload":"!!!!","payload":"aGk="}', None),
+    # ints: integer literals only; a wrong-typed member fails even before a good one
+    (b'{"Type":1.0,"ConnID":1}', None),
+    (b'{"Type":"1","ConnID":1}', None),
+    (b'{"Type":true}', None),
+    (b'{"Type":1,"ConnID":1e2}', None),
+    (b'{"ConnID":"x","connid":2,"Type":2}', None),
+    (b'{"Type":null,"type":2,"ConnID":7,"connid":null}', (2, 7, 0, None)),
+    (b'{"Type":2,"SeqNum":9223372036854775807}', (2, 0, 9223372036854775807, None)),
+    (b'{"Type":2,"SeqNum":9223372036854775808}', None),
+    (b'{"Type":2,"SeqNum":-3}', (2, 0, -3, None)),
+    # absent Type is MsgConnect (0); unknown types decode (the endpoints ignore them)
+    (b'{"ConnID":0,"SeqNum":0}', (0, 0, 0, None)),
+    (b'{"Type":7,"ConnID":1}', (7, 1, 0, None)),
+    (b'{"tYpE":2,"cOnNiD":5,"seqnum":6,"X":[1,{"y":null}]}', (2, 5, 6, None)),
+    (b'[1,2]', None),
+    (b'{"Type":1,"X":NaN}', None),
+]
+
+
+def _lsp_python(doc):
+    from lsp.message import Message
+    try:
+        m = Message.unmarshal(doc)
+    except (ValueError, TypeError):
+        return None
+    return (int(m.Type), m.ConnID, m.SeqNum, m.Payload)
+
+
+def _lsp_native(exe, docs):
+    out = subprocess.run([exe, "lsp"], input="\n".join(d.hex() for d in docs) + "\n", capture_output=True,
+                         text=True, timeout=30, check=True).stdout.splitlines()
+    res = []
+    for ln in out:
+        if ln == "ERR":
+            res.append(None)
+        else:
+            _, t, c, q, p = ln.split(" ")
+            res.append((int(t), int(c), int(q), None if p == "-" else bytes.fromhex(p)))
+    return res
+
+
+def test_python_lsp_reader_decodes_like_go():
+    for doc, want in LSP_CASES:
+        assert _lsp_python(doc) == want, doc
+
+
+def test_native_lsp_reader_decodes_like_go(probe):
+    got = _lsp_native(probe, [d for d, _ in LSP_CASES])
+    for (doc, want), g in zip(LSP_CASES, got):
+        assert g == want, doc
+
+
+def test_lsp_readers_round_trip_and_agree_on_random_frames(probe):
+    """Frames the writers produce read back exactly, and random mutations of them (case
+    changes, duplicated keys, nulls, junk base64) decode the same in both readers."""
+    import random
+    from lsp.message import Message, MsgType
+    rng = random.Random(11)
+    docs = []
+    for _ in range(300):
+        m = Message(rng.choice(list(MsgType)), rng.randrange(0, 1 << 31), rng.randrange(0, 1 << 31),
+                    None if rng.random() < 0.3 else bytes(rng.randrange(256) for _ in range(rng.randrange(0, 40))))
+        raw = m.marshal()
+        assert Message.unmarshal(raw) == m
+        s = raw.decode()
+        k = rng.randrange(5)
+        if k == 0:
+            s = s.replace('"Payload"', '"payload"')
+        elif k == 1:
+            s = s[:-1] + ',"PAYLOAD":null}'
+        elif k == 2:
+            s = s[:-1] + ',"payload":"' + rng.choice(["aGk=", "aG", "a=Gk", "@@@@", ""]) + '"}'
+        elif k == 3:
+            s = s[:-1] + ',"seqnum":' + rng.choice(["1", "-1", "1.5", '"1"', "null"]) + "}"
+        docs.append(s.encode())
+    assert _lsp_native(probe, docs) == [_lsp_python(d) for d in docs]
