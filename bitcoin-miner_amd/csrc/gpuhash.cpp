@@ -495,7 +495,7 @@ static int run_slice(gpuhash_ctx* ctx, const uint8_t* msg, size_t msg_len, uint6
                      uint64_t upper, uint32_t rchunk, uint64_t& bh, uint64_t& bn, bool& any,
                      gpuhash_stats& st) {
     const int n = (int)ctx->devs.size();
-    std::vector<Shard> sh = shard_range(msg_len, lower, upper, n);
+    std::vector<Shard> sh = shard_range(msg_len, lower, upper, n, ctx->policy);
     for (auto& d : ctx->devs) { d.used = false; d.rc = GPUHASH_OK; d.kernel_ms = 0; d.launches = 0; }
     if (n == 1) {
         ctx->devs[0].rc = dev_run(ctx->devs[0], msg, msg_len, lower, upper, rchunk, 0, nullptr, ctx->policy);

@@ -68,13 +68,22 @@ int gpuhash_plan_all(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t 
 int gpuhash_shard(uint64_t msg_len, uint64_t lower, uint64_t upper, int n, uint64_t* lo,
                   uint64_t* hi, int* empty) {
     if (lower > upper || n < 1) return -1;
-    std::vector<Shard> s = shard_range(msg_len, lower, upper, n);
+    std::vector<Shard> s = shard_range(msg_len, lower, upper, n, g_policy);
     for (int i = 0; i < n; i++) {
         lo[i] = s[(size_t)i].lo;
         hi[i] = s[(size_t)i].hi;
         empty[i] = s[(size_t)i].empty;
     }
     return 0;
+}
+
+// The cost model's price of the plan of [lower, upper] (plan_cost): what a shard of that
+// range really costs under the layouts plan_range picks for it.
+double gpuhash_plan_cost(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper) {
+    if (lower > upper) return -1;
+    std::vector<Launch> v;
+    plan_range(msg, len, lower, upper, v, 0, g_policy);
+    return plan_cost(v);
 }
 
 // Replays the kernel's per-nonce computation from launch `idx`'s descriptor.

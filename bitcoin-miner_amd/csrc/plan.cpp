@@ -9,6 +9,7 @@
 #include "plan.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 
 namespace gpuhash {
@@ -206,6 +207,34 @@ bool tail_layout(uint64_t m, int d, const GroupLayout& g, GroupLayout& out) {
     return true;
 }
 
+// The layout plan_range runs digit group d with when the search covers `span` of its
+// nonces (0 = all of them / unknown): layout_for under the policy's base, then the
+// tail-digit layout when it qualifies and the policy and span allow it.  Returns whether
+// the tail-digit layout was taken (`g` is then that layout).
+bool group_layout(uint64_t len, int d, uint64_t span, int policy, GroupLayout& g) {
+    g = layout_for(len, d, span, policy & kLayoutMask);
+    GroupLayout gt;
+    const bool tail = !(policy & kLayoutTailNever) &&
+                      ((policy & kLayoutTailAlways) || span == 0 || span >= kTailMinSpan) &&
+                      tail_layout(len, d, g, gt);
+    if (tail) g = gt;
+    return tail;
+}
+
+// Relative VALU work per nonce of a layout: one final-block compression, +0.7 for the
+// extra constant block, + the per-lane block B-1 compression amortised over R nonces.
+// (measured per-layout rates, profiles/r01_layout_sweep.jsonl: plain 32-39 GH/s,
+// uniform-schedule C2 ~45, extra padding block ~20.5)
+double layout_cost(const GroupLayout& g) {
+    double c = 1.0;
+    if (g.EX) c += 0.7;
+    if (g.C2 == 2 || g.C2 == 3 || (g.C2 == 1 && g.J == 0)) c = 0.75;
+    if (g.C2 == 3) return c + 0.6 / (double)pow10u(g.s);  // per-row schedule over the loop
+    if (g.C2) c += 0.9 / (double)pow10u(g.q);
+    else c += 0.2 / (double)std::min<uint64_t>(pow10u(g.q), 100);
+    return c;
+}
+
 inline uint32_t low_bytes_mask(int nbytes) {
     if (nbytes <= 0) return 0u;
     if (nbytes >= 4) return 0xFFFFFFFFu;
@@ -386,12 +415,10 @@ void plan_range(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper
         b = std::min(b, upper);
         if (a > b) continue;
         const uint64_t span = b - a == UINT64_MAX ? 0 : b - a + 1;
-        GroupLayout g = layout_for(len, d, span, policy & kLayoutMask);
-        GroupLayout gt;
-        const bool tail = !(policy & kLayoutTailNever) &&
-                          ((policy & kLayoutTailAlways) || span == 0 || span >= kTailMinSpan) &&
-                          tail_layout(len, d, g, gt);
+        GroupLayout g;
+        const bool tail = group_layout(len, d, span, policy, g);
         if (tail) {
+            const GroupLayout& gt = g;
             // ten launch sets, one per last digit t: k = nonce / 10 over the nonces = t (mod
             // 10) of [a, b] (a >= 10^(d-1) >= 10, so every k has d-1 digits)
             for (uint32_t t = 0; t < 10; t++) {
@@ -448,36 +475,40 @@ void plan_range(const uint8_t* msg, uint64_t len, uint64_t lower, uint64_t upper
     }
 }
 
-double group_cost(uint64_t msg_len, int d) {
-    GroupLayout g = layout_for(msg_len, d);
-    // a whole digit group spans far more than kTailMinSpan nonces: a one-digit last word
-    // runs as tail-digit launches, whose loop is the previous word's 10^4 values
-    GroupLayout gt;
-    if (tail_layout(msg_len, d, g, gt)) g = gt;
-    // relative VALU work per nonce: one final-block compression, +0.7 for the extra
-    // constant block, + the per-lane block B-1 compression amortised over R nonces.
-    // (measured per-layout rates, profiles/r01_layout_sweep.jsonl: plain 32-39 GH/s,
-    // uniform-schedule C2 ~45, extra padding block ~20.5)
-    double c = 1.0;
-    if (g.EX) c += 0.7;
-    if (g.C2 == 2 || g.C2 == 3 || (g.C2 == 1 && g.J == 0)) c = 0.75;
-    if (g.C2 == 3) return c + 0.6 / (double)pow10u(g.s);  // per-row schedule over the loop
-    if (g.C2) c += 0.9 / (double)pow10u(g.q);
-    else c += 0.2 / (double)std::min<uint64_t>(pow10u(g.q), 100);
+double group_cost(uint64_t msg_len, int d, uint64_t span, int policy) {
+    GroupLayout g;
+    group_layout(msg_len, d, span, policy, g);
+    return layout_cost(g);
+}
+
+double plan_cost(const std::vector<Launch>& plan) {
+    double c = 0;
+    for (const Launch& l : plan) {
+        GroupLayout g{};
+        g.d = l.d; g.J = l.J; g.q = l.q; g.s = l.s; g.C2 = l.C2; g.EX = l.EX;
+        c += (double)((l.hi - l.lo) / l.stride + 1) * layout_cost(g);
+    }
     return c;
 }
 
-std::vector<Shard> shard_range(uint64_t msg_len, uint64_t lower, uint64_t upper, int n) {
+std::vector<Shard> shard_range(uint64_t msg_len, uint64_t lower, uint64_t upper, int n, int policy) {
     std::vector<Shard> sh((size_t)std::max(n, 1));
     if (n <= 1) { sh[0] = {lower, upper, 0}; return sh; }
     struct G { uint64_t a, b; long double w; };
     std::vector<G> gs;
     long double total = 0;
+    // A shard runs its part of a digit group with the layout plan_range picks for THAT
+    // part (the tail-digit launches and the J = 1 straddle choice depend on the span the
+    // call covers): each group is priced at the span a shard typically holds
+    // of it, min(the group's span in the range, the range / n).
+    const long double per_shard = ((long double)(upper - lower) + 1.0L) / (long double)n;
     for (int d = num_digits(lower); d <= num_digits(upper); d++) {
         uint64_t a = d == 1 ? 0 : pow10u(d - 1), b = d == 20 ? UINT64_MAX : pow10u(d) - 1;
         a = std::max(a, lower); b = std::min(b, upper);
         if (a > b) continue;
-        long double w = (long double)group_cost(msg_len, d);
+        const long double est = std::min(((long double)(b - a) + 1.0L), std::ceil(per_shard));
+        const uint64_t span = est >= 18446744073709551616.0L ? 0 : (uint64_t)est;
+        long double w = (long double)group_cost(msg_len, d, span, policy);
         gs.push_back({a, b, w});
         total += ((long double)(b - a) + 1.0L) * w;
     }

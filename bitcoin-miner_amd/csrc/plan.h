@@ -137,10 +137,16 @@ struct Shard {
 // Splits [lower, upper] into n contiguous shards of about equal estimated cost
 // (nonce count weighted by the layout's per-nonce cost).  Used to spread one search
 // over the devices of a context (static contiguous shards).
-std::vector<Shard> shard_range(uint64_t msg_len, uint64_t lower, uint64_t upper, int n);
+// `policy` = the layout policy the shards will be planned with (plan_range).
+std::vector<Shard> shard_range(uint64_t msg_len, uint64_t lower, uint64_t upper, int n,
+                               int policy = kLayoutAuto);
 
-// Relative per-nonce cost of digit group d for a message of msg_len bytes.
-double group_cost(uint64_t msg_len, int d);
+// Relative per-nonce cost of digit group d for a message of msg_len bytes, when a call
+// covers `span` of its nonces (0 = the whole group) under layout policy `policy`.
+double group_cost(uint64_t msg_len, int d, uint64_t span = 0, int policy = kLayoutAuto);
+
+// The same cost model summed over a plan's launches (nonces x their layout's cost).
+double plan_cost(const std::vector<Launch>& plan);
 
 // Host SHA-256 pieces used for midstates (not a hashing path of its own).
 void sha256_compress(uint32_t st[8], const uint32_t w16[16]);

@@ -18,6 +18,7 @@ LIBDIR = os.path.join(ROOT, "bitcoin-miner_amd", "lib")
 # tests/test_sanitizers.py reruns this module against the ASan/UBSan build
 HC = os.environ.get("GPUHASH_HOSTCHECK_LIB") or os.path.join(LIBDIR, "libgpuhash_hostcheck.so")
 U64 = (1 << 64) - 1
+M120 = (b"The quick brown fox jumps over the lazy dog. " * 3)[:120]
 u64 = ctypes.c_uint64
 
 
@@ -41,6 +42,8 @@ def hc():
     lib.hostcheck_desc_hash.argtypes = [cp, u64, u64, u64, u32, ctypes.c_int, u64, ctypes.POINTER(u64)]
     lib.gpuhash_shard.argtypes = [u64, u64, u64, ctypes.c_int, ctypes.POINTER(u64),
                                   ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_int)]
+    lib.gpuhash_plan_cost.argtypes = [cp, u64, u64, u64]
+    lib.gpuhash_plan_cost.restype = ctypes.c_double
     lib.hostcheck_set_layout_policy.argtypes = [ctypes.c_int]
     lib.hostcheck_set_layout_policy(AUTO)
     return lib
@@ -293,6 +296,33 @@ def test_shards_balance_config4(hc):
     s = shards(hc, 8, 0, (1 << 40) - 1, 8)
     counts = [hi - lo + 1 for lo, hi in s]
     assert max(counts) / min(counts) < 1.03
+
+
+def _shard_costs(hc, msg, a, b, n):
+    return [hc.gpuhash_plan_cost(msg, len(msg), lo, hi) for lo, hi in
+            (x for x in shards(hc, len(msg), a, b, n) if x is not None)]
+
+
+@pytest.mark.parametrize("policy", [AUTO, AUTO | 16, AUTO | 32])
+def test_shard_costs_follow_each_shards_plan(hc, policy):
+    """a shard is priced by the layouts ITS plan uses.  Mid-size ranges (2^33 to
+    2^36 over 8 devices) give shards below the tail-digit span (2^33), so their 8- and
+    12-digit 'bradfitz' nonces run the plain one-digit-loop layout, not the tail-digit
+    launches a whole digit group would get; under TAIL_ALWAYS / TAIL_NEVER the plans follow
+    the flag.  Across a digit boundary whose two groups run different layouts, the cost
+    of every shard's own plan (plan_cost, the same model) stays within 0.5% of the mean."""
+    hc.hostcheck_set_layout_policy(policy)
+    try:
+        for msg, a, b in [(b"bradfitz", 10 ** 11 - (1 << 34), 10 ** 11 + (1 << 34)),
+                          (b"bradfitz", 10 ** 11 - (1 << 32), 10 ** 11 + (1 << 35)),
+                          (b"bradfitz", 10 ** 7 - (1 << 22), 10 ** 7 + (1 << 33)),
+                          (M120[:45], 10 ** 9 - (1 << 29), 10 ** 9 + (1 << 33)),
+                          (b"bradfitz", 0, (1 << 40) - 1)]:
+            costs = _shard_costs(hc, msg, a, b, 8)
+            mean = sum(costs) / len(costs)
+            assert max(costs) / mean < 1.005 and min(costs) / mean > 0.995, (msg, a, b, costs)
+    finally:
+        hc.hostcheck_set_layout_policy(AUTO)
 
 
 @pytest.mark.parametrize("mlen", [61, 62, 125, 126])
