@@ -15,7 +15,7 @@ the GPU) -- with config 5's LSP parameters and 10% drops on every role:
   a mostly-sleeping loop responsive);
 * test_stalled_server_is_named: the negative control -- the server process stopped
   (SIGSTOP) for 2.6 s, longer than 10 epochs: the clients print Disconnected, their stderr
-  names 10 silent epochs with the server last heard >= 2 s earlier, and the server's own
+  names 10 silent epochs with the server last heard >= 9 epochs (1.8 s) earlier, and the server's own
   loop reports the epoch it fired >= 2 s late.  That is the signature a starved server
   leaves, which the full-size GPU test now records.
 """
@@ -151,6 +151,6 @@ def test_stalled_server_is_named(procs, tmp_path):
     for out, err in res:
         assert out.strip() == "Disconnected", (out, err[-800:])
         m = re.search(r"connection lost \(10 silent epochs, peer last heard (\d+) ms ago", err)
-        assert m and int(m.group(1)) >= 1900, err[-800:]
+        assert m and int(m.group(1)) >= 1750, err[-800:]  # 10 epochs counted from the next one
     lines = [int(x) for x in re.findall(r"lsp-server\[\d+\]: epoch fired (\d+) ms late", log)]
     assert lines and max(lines) >= 2000, log[-1500:]
