@@ -70,7 +70,13 @@ CFG5_CLIENTS = [f"client-{i:02d}" for i in range(16)]
 HUGE = [(f"cfg5_{c}_2p36", c.encode(), 0, 1 << 36, "config 5: one client's whole request")
         for c in CFG5_CLIENTS] + [
     ("cfg4_bradfitz_2p40", b"bradfitz", 0, (1 << 40) - 1, "config 4: [0, 2^40) of bradfitz"),
-]
+] + [
+    # the timed step of bench.py's config 2 at N = 2, 4, 8 GPUs searches [0, N * 2^32) (weak
+    # scaling, rank r on [r * 2^32, (r + 1) * 2^32)), so the driver's scaling lines are
+    # golden-checked too; and config 4's one-GPU step, [0, 2^37)
+    (f"cfg2_bradfitz_{n}gpu", b"bradfitz", 0, (n << 32) - 1, f"config 2's timed step at N = {n}")
+    for n in (2, 4, 8)
+] + [("cfg4_bradfitz_2p37", b"bradfitz", 0, (1 << 37) - 1, "config 4's timed step at N = 1")]
 
 
 def run_huge(names: list[str], threads: int) -> None:
