@@ -4,7 +4,9 @@
 Draws (message, range) cases across message lengths 0-300 (plus a few 1-4 KB), every
 digit count 1-20, ranges of 1 to ~2e6 nonces placed at random or straddling a digit-count
 boundary, under every layout policy (a third of the cases with the tail-digit launches
-forced), and compares gpuhash_min with the C oracle's scan.
+forced), and compares gpuhash_min with the C oracle's scan.  Since round 5 a fifth of the
+cases run on a context with 2, 3 or 8 entries of the one GPU, so the in-process shard cuts
+(the cost model of plan.cpp shard_range, priced per shard span and policy) are soaked too.
 Prints one JSON line per 100 cases and a summary; exits 1 on the first mismatch.
 """
 import json
@@ -46,10 +48,15 @@ def case():
 
 
 t0 = time.time()
-count = nonces = 0
-with gpuhash.Engine([0]) as eng:
+count = nonces = multi_cases = 0
+multis = [gpuhash.Engine([0] * k) for k in (2, 3, 8)]
+with gpuhash.Engine([0]) as one:
     while time.time() - t0 < seconds:
         m, lo, hi = case()
+        eng = one
+        if rng.random() < 0.2:
+            eng = rng.choice(multis)
+            multi_cases += 1
         policy = rng.choice([gpuhash.LAYOUT_AUTO, gpuhash.LAYOUT_UNIFORM, gpuhash.LAYOUT_CLASSIC,
                              gpuhash.LAYOUT_LANETABLE])
         # round 4: the tail-digit launches (AUTO takes them only above 2^33 nonces per
@@ -63,10 +70,14 @@ with gpuhash.Engine([0]) as eng:
         nonces += hi - lo + 1
         if got != want:
             print(json.dumps({"MISMATCH": True, "msg_hex": m.hex(), "lower": lo, "upper": hi,
-                              "policy": policy, "got": list(got), "want": list(want)}), flush=True)
+                              "policy": policy, "entries": eng.ndevices, "got": list(got),
+                              "want": list(want)}), flush=True)
             sys.exit(1)
         if count % 100 == 0:
             print(json.dumps({"cases": count, "nonces": nonces, "elapsed_s": round(time.time() - t0, 1)}),
                   flush=True)
-print(json.dumps({"summary": True, "cases": count, "nonces": nonces, "mismatches": 0, "seed": seed,
+for e in multis:
+    e.close()
+print(json.dumps({"summary": True, "cases": count, "multi_device_cases": multi_cases, "nonces": nonces,
+                  "mismatches": 0, "seed": seed, "build_id": gpuhash.build_id(),
                   "elapsed_s": round(time.time() - t0, 1)}), flush=True)
