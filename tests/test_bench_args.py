@@ -173,8 +173,13 @@ def test_timed_step_is_checked_against_the_goldens():
     c3 = bench.step_check(bench.M120, w3, (0, 0))
     assert c3["golden_names"] and len(c3["golden_names"]) == 2 and c3["matches_golden"] is False
     assert bench.step_check(bench.M120, w3, tuple(c3["golden"]))["matches_golden"] is True
-    # no golden for config 2 over 2 GPUs: skipped, and says why
-    sk = bench.step_check(bench.MSG, [(0, (2 << 32) - 1)], (1, 2))
+    # config 2's timed step at N = 2, 4, 8 GPUs ([0, N * 2^32)) has a golden since round 5;
+    # N = 3 does not: skipped, and says why
+    for n in (2, 4, 8):
+        merged = bench.merge_windows(w for r in range(n) for w in bench.CONFIGS["2"]["windows"](r))
+        assert bench.step_check(bench.MSG, merged, (0, 0))["golden_names"] == [f"cfg2_bradfitz_{n}gpu"]
+    assert bench.step_check(bench.MSG, [(0, (1 << 37) - 1)], (0, 0))["golden_names"] == ["cfg4_bradfitz_2p37"]
+    sk = bench.step_check(bench.MSG, [(0, (3 << 32) - 1)], (1, 2))
     assert sk["matches_golden"] is None and "no committed golden" in sk["reason"]
     bench.search_exit({"matches_golden": None}, [])  # a skipped check does not fail the run
 

@@ -3,8 +3,9 @@ HIP engine replaced by an oracle-backed stand-in and torch.cuda by a two-GPU fak
 code the driver's N > 1 scaling run executes (timed steps, the ranks' search leg with
 its gloo merge, rank 0's in-process repeat over all GPUs, the device/PCI checks, the one
 JSON line) with no GPU.  The stand-in is test infrastructure: it hashes with the C
-oracle on the search range (config 1's [0, 9999], whose golden is committed) and returns
-placeholder results for the 2^32 step windows, which the oracle could not scan."""
+oracle on the search range (config 1's [0, 9999], whose golden is committed) and answers
+the 2^32 step windows, which the oracle could not scan here, from the committed CPU
+goldens that cover them."""
 import io
 import json
 import os
@@ -41,6 +42,9 @@ def _worker(rank, world, port, ndev, share, q, pinned=False):
     import hash_oracle
     import bench
     oracle = hash_oracle.load_c_oracle()
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+        goldens = json.load(f)["ranges"]
 
     class FakeEngine:
         """gpuhash.Engine's surface, oracle-backed on small ranges."""
@@ -57,7 +61,13 @@ def _worker(rank, world, port, ndev, share, q, pinned=False):
                          for i, c in enumerate(cuts) if c is not None]
             if hi - lo < 1_000_000:
                 return oracle.min(msg, lo, hi)
-            return (lo * 2654435761 % (1 << 64), lo)  # placeholder for the 2^32 step windows
+            # a 2^32 step window: the committed CPU golden of a range that contains it and
+            # whose winner lies inside it is this window's answer too (its min over the
+            # superset is attained here)
+            for g in goldens:
+                if g["msg_hex"] == msg.hex() and g["lower"] <= lo and hi <= g["upper"] and lo <= g["nonce"] <= hi:
+                    return (g["hash"], g["nonce"])
+            raise AssertionError(f"no golden covers [{lo}, {hi}]")
 
         def launches(self):
             return list(self.recs)
@@ -133,8 +143,8 @@ def test_two_ranks_on_two_gpus_search_leg_and_inproc_repeat():
     sc = s["scaling"]
     assert sc["shard"] == 0 and sc["windows"] == s["shards"][0]["windows"]
     assert sc["t_all_s"] == s["seconds"] and sc["scaling_efficiency"] > 0
-    # the timed step spans [0, 2^33): no committed golden, so its check is skipped, with why
-    assert line["matches_golden"] is None and "no committed golden" in line["result_check"]["reason"]
+    # the timed step spans [0, 2^33): checked against config 2's N = 2 golden
+    assert line["matches_golden"] is True and line["result_check"]["golden_names"] == ["cfg2_bradfitz_2gpu"]
 
 
 def test_ranks_pinned_to_one_visible_gpu_each():

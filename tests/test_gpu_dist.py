@@ -115,8 +115,8 @@ def test_bench_inproc_two_shards_on_one_gpu(engine):
     # the timed step's shard rates are per step, near the kernel rate
     assert all(x["nonces_hashed"] == x["nonces"] for x in line["shards"])  # one step here
     assert all(x["kernel_GHs"] > 5 for x in line["shards"])
-    # [0, 2^33) has no committed golden: the step check says it was skipped
-    assert line["matches_golden"] is None and "no committed golden" in line["result_check"]["reason"]
+    # the timed step's [0, 2^33) is checked against its CPU golden (config 2 at N = 2)
+    assert line["matches_golden"] is True and line["result_check"]["golden_names"] == ["cfg2_bradfitz_2gpu"]
 
 
 def test_bench_gpus_above_visible_fails_loudly():
@@ -154,6 +154,7 @@ def test_bench_torchrun_two_ranks_on_one_gpu(engine):
     assert si["matches_golden"] is True and si["devices"] == [0, 0]
     assert [x["shard"] for x in si["shards"]] == [0, 1] and bench.tiles(si["shards"], 0, (1 << 32) - 1)
     assert 0.3 < s["scaling"]["scaling_efficiency"] < 0.8  # two ranks share the GPU
+    assert line["matches_golden"] is True and line["result_check"]["golden_names"] == ["cfg2_bradfitz_2gpu"]
     # without GPUHASH_SHARE_GPU, two ranks on a 1-GPU box must fail loudly: refused at
     # start, or -- when a *_VISIBLE_DEVICES variable leaves each process one GPU, which
     # bench.py accepts as one GPU per rank -- by the PCI check once both ranks report the
