@@ -75,6 +75,7 @@ def test_roofline_of_the_dominant_kernel(monkeypatch):
     assert r["achieved"] == pytest.approx(want, rel=1e-3)
     assert r["frac"] == pytest.approx(want / bench.VALU_PEAK_T, rel=1e-3)
     assert r["traffic"] is None and r["issued_frac"] is None
+    assert r["target_frac"] == 0.70 and r["target_met"] is (r["frac"] >= 0.70)
 
 
 # ---- the 2^40 search leg ----
