@@ -4,8 +4,8 @@ lsp.Message.unmarshal (lsp/message.go:17-22), and restated in C++ by csrc/lsp_na
 
   go_object   json.loads object hook: keys select struct fields ignoring (ASCII) case, and
               EVERY matching member is kept in document order (Go decodes each of them)
-  field       the value Unmarshal leaves in a field: members in order, null skipped (or
-              resetting, for slices), a wrong-typed member fails the message
+  field       the value Unmarshal leaves in a scalar field: members in order, null
+              skipped, a wrong-typed member fails the message
   IntLit      an integer literal that keeps its text (ParseUint refuses "-0")
   go_utf8     invalid UTF-8 as one U+FFFD per byte (utf8.DecodeRune)
   loads       json.loads with these hooks; NaN / Infinity refused
@@ -38,16 +38,14 @@ def go_object(pairs) -> dict:
     return out
 
 
-def field(d: dict, key: str, ok, default, null_resets: bool = False):
-    """The value json.Unmarshal leaves in field `key`: each matching member in order, the
-    last accepted one wins; null is a no-op, except for a slice / map / pointer field
-    (`null_resets`), which null sets back to nil (= `default`); `ok(v)` False for any member
-    -> ValueError (Go keeps the first UnmarshalTypeError and returns it)."""
+def field(d: dict, key: str, ok, default):
+    """The value json.Unmarshal leaves in a scalar field `key` (int, uint64, string): each
+    matching member in order, null skipped (a no-op for these kinds; a []byte field, where
+    null resets to nil, is read by lsp.message), the last accepted one wins; `ok(v)` False
+    for any member -> ValueError (Go keeps the first UnmarshalTypeError and returns it)."""
     val = default
     for v in d.get(key.translate(_FOLD), ()):
         if v is None:
-            if null_resets:
-                val = default
             continue
         if not ok(v):
             raise ValueError(f"json: cannot unmarshal {v!r} into Go struct field Message.{key}")
