@@ -29,7 +29,7 @@ class Members(list):
 def go_object(pairs) -> dict:
     """json.loads object hook with encoding/json's field matching: a key selects the
     struct field whose name equals it ignoring (ASCII) case.  Go decodes EVERY such member
-    in order into the field, so all of them are kept (case-folded key -> _Members): a later
+    in order into the field, so all of them are kept (case-folded key -> Members): a later
     null leaves the field as an earlier member set it, and a member of the wrong type fails
     the message even when a later one is fine (csrc/lsp_native.h jfields)."""
     out: dict = {}
