@@ -2,7 +2,7 @@
 # tools/gpu_session.sh STEP... -- runs GPU steps on the gpurun box, each under its own
 # time limit, logging to gpurun_out/.  A plain failure (exit 1, e.g. a failing test)
 # lets the next step run; a fault, abort, segfault, time limit or kill stops the session.
-# Steps: hostwait | c5diag | lsweep | inproc8s | dist8s | fma | cumask | family | inproc8c4 | valu | go | test | soak | smoke | bench | bench3 | bench4 | prof4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | pmc3 | pmc4 | sweep | variants | partial | regret | sys5
+# Steps: hostwait | c5diag | c5stream | c5poll | lsweep | inproc8s | dist8s | fma | cumask | family | inproc8c4 | valu | go | test | soak | smoke | bench | bench3 | bench4 | prof4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | pmc3 | pmc4 | sweep | variants | partial | regret | sys5
 set -u
 cd "$(dirname "$0")/.."
 OUT=gpurun_out
@@ -39,6 +39,9 @@ for step in "$@"; do
         smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
         hostwait) run hostwait 400 python -u tools/host_wait_probe.py --procs "${HW_PROCS:-8}" --modes "${HW_MODES:-stream,event,poll}" ;;
         c5diag) run c5diag${C5TAG:-} 400 env GPUHASH_DIAG_DIR="$OUT/c5${C5TAG:-}" python -u -m pytest tests/test_gpu_system.py -m gpu -x -v -s --timeout 300 --timeout-method thread -k config5_full_size ;;
+        c5stream) for i in $(seq 1 "${C5_REPEAT:-8}"); do
+                      run c5stream_$i 200 env GPUHASH_HOST_WAIT=stream GPUHASH_DIAG_DIR="$OUT/c5stream_$i" python -u -m pytest tests/test_gpu_system.py -m gpu -x -v -s --timeout 180 --timeout-method thread -k config5_full_size
+                  done ;;
         c5poll) run c5poll 400 env GPUHASH_HOST_WAIT=poll GPUHASH_DIAG_DIR="$OUT/c5poll" python -u -m pytest tests/test_gpu_system.py -m gpu -x -v -s --timeout 300 --timeout-method thread -k config5_full_size ;;
         benchwait) for i in 1 2; do for m in stream poll; do
                        run benchwait_${m}_$i 200 env GPUHASH_HOST_WAIT=$m python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --search off
