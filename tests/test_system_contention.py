@@ -52,14 +52,17 @@ class Procs:
     def __init__(self):
         self.ps = []
 
-    def start(self, argv, **env):
+    def start(self, argv, cpu=None, **env):
+        """`cpu`: pin the process (every thread it will start) to that one CPU from exec on."""
         e = dict(os.environ, **LSP, **{k: str(v) for k, v in env.items()})
-        p = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=e)
+        pin = None if cpu is None else (lambda: os.sched_setaffinity(0, {cpu}))
+        p = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=e,
+                             preexec_fn=pin)
         self.ps.append(p)
         return p
 
-    def py(self, prog, *args, **env):
-        return self.start([sys.executable, os.path.join(BIN, prog), *map(str, args)], **env)
+    def py(self, prog, *args, cpu=None, **env):
+        return self.start([sys.executable, os.path.join(BIN, prog), *map(str, args)], cpu=cpu, **env)
 
     def stop(self, p):
         if p.poll() is None:
@@ -97,14 +100,18 @@ def _hogs(cpu: int, n: int):
 def test_config5_shape_under_cpu_pressure(procs, tmp_path, oracle):
     miner = build_miner(tmp_path)
     port = free_port()
-    server = procs.py("server", port, GPUHASH_SERVER_LOG=1, GPUHASH_JOB_SIZE=1 << 21, **DROPS)
     cpu = sorted(os.sched_getaffinity(0))[-1]
-    os.sched_setaffinity(server.pid, {cpu})
+    server = procs.py("server", port, cpu=cpu, GPUHASH_SERVER_LOG=1, GPUHASH_JOB_SIZE=1 << 21, **DROPS)
     hogs = _hogs(cpu, 8)
     try:
         time.sleep(0.5)
         miners = [procs.start([miner, f"127.0.0.1:{port}"], **DROPS) for _ in range(4)]
         time.sleep(1.0)
+        # every thread of the server (its LSP loop included) runs on the contended CPU
+        for tid in os.listdir(f"/proc/{server.pid}/task"):
+            with open(f"/proc/{server.pid}/task/{tid}/status") as f:
+                allowed = [ln.split()[1] for ln in f if ln.startswith("Cpus_allowed_list")]
+            assert allowed == [str(cpu)], (tid, allowed)
         sampler = sysdiag.CgroupSampler()
         sampler.start()
         n = 1 << 22
