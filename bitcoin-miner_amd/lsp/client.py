@@ -74,6 +74,10 @@ class Client:
         self._conn.write_to(m.marshal())
 
     def _on_datagram(self, data: bytes, addr) -> None:
+        # only the server's datagrams: the reference's lspnet.DialUDP is a connected UDP
+        # socket, which the kernel filters by source (csrc/lsp_native.h does the same)
+        if addr != self._conn.peer:
+            return
         try:
             m = Message.unmarshal(data)
         except (ValueError, KeyError):

@@ -190,3 +190,28 @@ def test_duplicate_connect_same_address_keeps_one_connection():
     assert len(srv._conns) == 1
     c.Close()
     srv.Close()
+
+
+def test_client_hears_only_its_server():
+    """The reference's lspnet.DialUDP is a connected UDP socket, so a client reads only its
+    server's datagrams; a frame from any other address (here a Data frame carrying the
+    client's own conn ID and the next sequence number) is ignored, as csrc/lsp_native.h
+    does."""
+    import socket
+    from lsp.message import NewData
+    params = lsp.Params(**FAST)
+    srv = lsp.NewServer(0, params)
+    c = lsp.NewClient(f"127.0.0.1:{srv.port}", params)
+    rogue = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    rogue.bind(("127.0.0.1", 0))
+    for _ in range(3):
+        rogue.sendto(NewData(c.ConnID(), 1, b"forged").marshal(), ("127.0.0.1", c._conn.local_addr()[1]))
+    time.sleep(0.2)
+    srv.Write(c.ConnID(), b"real")
+    assert c.Read() == b"real"
+    rogue.close()
+    c.Close()
+    try:
+        srv.Close()
+    except lsp.LSPError:
+        pass
