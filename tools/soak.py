@@ -6,7 +6,9 @@ digit count 1-20, ranges of 1 to ~2e6 nonces placed at random or straddling a di
 boundary, under every layout policy (a third of the cases with the tail-digit launches
 forced), and compares gpuhash_min with the C oracle's scan.  Since round 5 a fifth of the
 cases run on a context with 2, 3 or 8 entries of the one GPU, so the in-process shard cuts
-(the cost model of plan.cpp shard_range, priced per shard span and policy) are soaked too.
+(the cost model of plan.cpp shard_range, priced per shard span and policy) are soaked too,
+and a tenth also compare every nonce's hash (gpuhash_hash_range, the kernels' MODE 1) over
+up to 2^16 nonces of the case with the oracle's.
 Prints one JSON line per 100 cases and a summary; exits 1 on the first mismatch.
 """
 import json
@@ -48,7 +50,7 @@ def case():
 
 
 t0 = time.time()
-count = nonces = multi_cases = 0
+count = nonces = multi_cases = per_nonce = 0
 multis = [gpuhash.Engine([0] * k) for k in (2, 3, 8)]
 with gpuhash.Engine([0]) as one:
     while time.time() - t0 < seconds:
@@ -73,11 +75,22 @@ with gpuhash.Engine([0]) as one:
                               "policy": policy, "entries": eng.ndevices, "got": list(got),
                               "want": list(want)}), flush=True)
             sys.exit(1)
+        if rng.random() < 0.1:  # per-nonce parity over the first <= 2^16 nonces of the case
+            k = min(hi - lo + 1, 1 << 16)
+            g = eng.hash_range(m, lo, k)
+            w = oracle.hash_range(m, lo, k)
+            per_nonce += k
+            if not (g == w).all():
+                bad = int((g != w).argmax())
+                print(json.dumps({"MISMATCH": True, "per_nonce": True, "msg_hex": m.hex(), "nonce": lo + bad,
+                                  "policy": policy, "got": int(g[bad]), "want": int(w[bad])}), flush=True)
+                sys.exit(1)
         if count % 100 == 0:
             print(json.dumps({"cases": count, "nonces": nonces, "elapsed_s": round(time.time() - t0, 1)}),
                   flush=True)
 for e in multis:
     e.close()
 print(json.dumps({"summary": True, "cases": count, "multi_device_cases": multi_cases, "nonces": nonces,
+                  "per_nonce_hashes_compared": per_nonce,
                   "mismatches": 0, "seed": seed, "build_id": gpuhash.build_id(),
                   "elapsed_s": round(time.time() - t0, 1)}), flush=True)
