@@ -525,22 +525,29 @@ def search_line(res, dt: float, n: int, lo: int, hi: int, mode: str, devices, sh
             "matches_golden": (tuple(res) == want) if want else None, "shards": shards}
 
 
-def alone_rerun(eng, row: dict, t_all: float, barrier) -> dict:
+def alone_rerun(make_engine, row: dict, t_all: float, barrier) -> dict:
     """Same-run scaling evidence: shard 0's exact window(s) of the
     N-device search, searched again ALONE on its device with the same engine code, after
     every other device has gone idle.  Perfect scaling means the N-device search took as
     long as its shard 0 takes alone, so scaling_efficiency = t_alone / t_all (shards are
     cost-balanced, so shard 0 stands for each of them).  The driver runs one N at a time;
-    this puts a same-run baseline into every N > 1 line."""
-    barrier()
+    this puts a same-run baseline into every N > 1 line.  It is evidence only: a host-side
+    failure is recorded in the object instead of ending the run (under torchrun the other
+    ranks wait at a barrier for this one), like rank 0's in-process repeat."""
     launches = []
-    t0 = time.perf_counter()
-    for lo, hi in row["windows"]:
-        eng.min(MSG, lo, hi)
-        launches += eng.launches()
-    barrier()
-    t_alone = time.perf_counter() - t0
-    eng.close()
+    try:
+        eng = make_engine()
+        barrier()
+        t0 = time.perf_counter()
+        for lo, hi in row["windows"]:
+            eng.min(MSG, lo, hi)
+            launches += eng.launches()
+        barrier()
+        t_alone = time.perf_counter() - t0
+        eng.close()
+    except Exception as e:  # noqa: BLE001 -- see above
+        return {"shard": row["shard"], "device": row["device"], "windows": row["windows"],
+                "error": f"{type(e).__name__}: {e}"}
     return {"shard": row["shard"], "device": row["device"], "windows": row["windows"],
             "t_alone_s": round(t_alone, 3), "t_all_s": round(t_all, 3),
             "scaling_efficiency": round(t_alone / t_all, 4) if t_all > 0 else None,
@@ -650,7 +657,7 @@ def main_inproc(args, devs: list[int]) -> None:
             problems.append("the search's shard windows do not tile its range")
         out["search_2p40"] = search_line(sres, sdt, n, lo, hi, "inproc", devs, rows)
         if n > 1 and rows:
-            out["search_2p40"]["scaling"] = alone_rerun(gpuhash.Engine([devs[0]]), rows[0], sdt, barrier)
+            out["search_2p40"]["scaling"] = alone_rerun(lambda: gpuhash.Engine([devs[0]]), rows[0], sdt, barrier)
     if problems:
         out["device_check"] = problems
     if n == 1:
@@ -748,7 +755,8 @@ def main_ranks(args, world: int, rank: int, local: int) -> None:
         if world > 1:
             barrier()
             if rank == 0 and srows:
-                alone = alone_rerun(gpuhash.Engine([local]), srows[0], sdt, lambda: torch.cuda.synchronize(dev))
+                alone = alone_rerun(lambda: gpuhash.Engine([local]), srows[0], sdt,
+                                    lambda: torch.cuda.synchronize(dev))
             barrier()
     pci = pci_id(local)
     host = socket.gethostname()

@@ -214,7 +214,17 @@ def test_alone_rerun_reports_scaling_efficiency():
 
     eng = Eng()
     row = {"shard": 0, "device": 0, "windows": [[0, 99], [200, 299]]}
-    s = bench.alone_rerun(eng, row, 0.2, lambda: None)
+    s = bench.alone_rerun(lambda: eng, row, 0.2, lambda: None)
     assert eng.calls == [(0, 99), (200, 299)] and eng.closed
     assert s["t_alone_s"] >= 0.1 and s["scaling_efficiency"] == pytest.approx(s["t_alone_s"] / 0.2, rel=1e-2)
     assert s["alone_sclk_mhz"] == 2400.0
+
+
+def test_alone_rerun_records_a_failure_instead_of_raising():
+    """Under torchrun the other ranks wait at a barrier while rank 0 re-runs its window: a
+    host-side exception there must not end rank 0 (the others would hang), so it is
+    recorded, like the in-process repeat's."""
+    def boom():
+        raise RuntimeError("no device")
+    s = bench.alone_rerun(boom, {"shard": 0, "device": 0, "windows": [[0, 9]]}, 1.0, lambda: None)
+    assert s["error"] == "RuntimeError: no device" and "scaling_efficiency" not in s
