@@ -9,8 +9,10 @@ engine (gpuhash_min through the C ABI):
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import sys
+import time
 
 import lsp
 
@@ -40,11 +42,16 @@ def run(hostport: str, engine=None, params=None, on_client=None) -> int:
         on_client(c)
     engine = engine or open_engine()
     jobs = 0
+    # GPUHASH_MINER_JOBLOG=1: one stderr line per job (wall-clock receive/start/end and the
+    # engine's kernel ms), from which tools/system_bench.py measures how busy the GPU was
+    joblog = os.environ.get("GPUHASH_MINER_JOBLOG", "") not in ("", "0")
     try:
         c.Write(marshal(NewJoin()))
         while True:
             try:
-                m = unmarshal(c.Read())
+                raw = c.Read()
+                t_recv = time.time()
+                m = unmarshal(raw)
             except (ValueError, KeyError):
                 continue  # not a Message: ignore, like the server does
             if m.Type != MsgType.Request:
@@ -56,8 +63,10 @@ def run(hostport: str, engine=None, params=None, on_client=None) -> int:
                 c.Write(marshal(NewResult(*EMPTY_RESULT)))
                 continue
             # was: for n := m.Lower; n <= m.Upper; n++ { h := bitcoin.Hash(m.Data, n) ... }
+            t_start = time.time()
             try:
                 h, n = engine.min(m.Data, m.Lower, m.Upper)
+                t_end = time.time()
             except Exception as e:
                 if isinstance(e, (ValueError, TypeError)) or getattr(e, "is_argument_error", False):
                     # deterministic (EINVAL/ETOOLONG): no Result can be sent for this job,
@@ -77,6 +86,11 @@ def run(hostport: str, engine=None, params=None, on_client=None) -> int:
                 raise
             c.Write(marshal(NewResult(h, n)))
             jobs += 1
+            if joblog:
+                st = engine.stats() if hasattr(engine, "stats") else {}
+                tag = hashlib.sha1(m.Data.encode("utf-8", "surrogatepass")).hexdigest()[:12]
+                _log(f"job data={tag} lo={m.Lower} hi={m.Upper} recv={t_recv:.6f} start={t_start:.6f} "
+                     f"end={t_end:.6f} kernel_ms={st.get('kernel_ms', 0.0):.3f}")
     except lsp.LSPError as e:
         _log(f"server lost after {jobs} job(s): {e}")
         return 0  # server lost: shut down (p1.pdf p.15)

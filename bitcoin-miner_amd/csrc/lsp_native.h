@@ -642,8 +642,7 @@ class Conn {
 
     // a message from the peer; payloads that became deliverable in order go to `out`
     void on_message(const LspMsg& m, std::deque<std::string>& out) {
-        silent_ = 0;
-        last_heard_ = std::chrono::steady_clock::now();
+        heard();
         if (m.type == MsgAck) {
             if (unacked_.erase(m.seq)) pump();
             return;
@@ -663,10 +662,18 @@ class Conn {
         }
     }
 
-    // epoch actions; true when this epoch made the connection lost
+    // epoch actions; true when this epoch made the connection lost: K whole epochs passed
+    // without hearing from the peer (an epoch in which something arrived is not silent, as
+    // the reference's counter, lsp/client_impl.go:236-277; lsp/endpoint.py on_epoch)
     bool on_epoch() {
         if (lost_) return false;
-        if (++silent_ >= k_) {
+        if (heard_) {
+            silent_ = 0;
+            heard_ = false;
+        } else {
+            silent_++;
+        }
+        if (silent_ >= k_) {
             lost_ = true;
             const auto ago = std::chrono::duration_cast<std::chrono::milliseconds>(
                 std::chrono::steady_clock::now() - last_heard_).count();
@@ -680,7 +687,7 @@ class Conn {
         return false;
     }
     void heard() {
-        silent_ = 0;
+        heard_ = true;
         last_heard_ = std::chrono::steady_clock::now();
     }
 
@@ -689,7 +696,8 @@ class Conn {
     int w_, k_;
     std::function<void(const LspMsg&)> send_;
     bool lost_ = false, got_data_ = false;
-    int silent_ = 0;
+    bool heard_ = true;  // heard from the peer since the last epoch
+    int silent_ = 0;     // whole epochs since the peer was last heard
     std::chrono::steady_clock::time_point last_heard_ = std::chrono::steady_clock::now();
     std::string lost_reason_;
     long long next_seq_ = 1, expected_ = 1;
@@ -887,6 +895,7 @@ class Server {
         bool lost = false;  // the connection was lost (or closed); no payload
         std::string payload;
         std::string reason;  // for `lost`: why ("closed" for a flushed close)
+        bool timed_out = false;  // read_until: the deadline passed with nothing to return
     };
 
     explicit Server(const Params& p) : p_(p), udp_(true) {}
@@ -905,6 +914,29 @@ class Server {
     Event read() {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [this] { return !events_.empty(); });
+        Event e = std::move(events_.front());
+        events_.pop_front();
+        return e;
+    }
+
+    // read(), but returns an Event with timed_out set once steady_clock passes `deadline_s`
+    // (seconds since its epoch) with nothing to return; the bitcoin server wakes for its own
+    // timer this way (not in server_api.go)
+    Event read_until(double deadline_s) {
+        using clk = std::chrono::steady_clock;
+        const auto left = clk::time_point(std::chrono::duration_cast<clk::duration>(
+                              std::chrono::duration<double>(deadline_s))) - clk::now();
+        // waited on the system clock: libstdc++ waits on steady_clock deadlines with
+        // pthread_cond_clockwait, which ThreadSanitizer does not intercept (it then misses
+        // the mutex hand-over and reports races on events_); pthread_cond_timedwait it does
+        const auto deadline = std::chrono::system_clock::now() +
+                              std::chrono::duration_cast<std::chrono::system_clock::duration>(left);
+        std::unique_lock<std::mutex> lk(mu_);
+        if (!cv_.wait_until(lk, deadline, [this] { return !events_.empty(); })) {
+            Event t;
+            t.timed_out = true;
+            return t;
+        }
         Event e = std::move(events_.front());
         events_.pop_front();
         return e;

@@ -24,12 +24,17 @@
 // disconnected; a lost client's requests are dropped and late results ignored.  A
 // Request is served only if 0 <= Lower <= Upper <= 2^64-1 and Data fits the engine;
 // otherwise the client's connection is closed.  stdout is never written.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <deque>
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -41,6 +46,18 @@ namespace {
 using lspn::BtcMsg;
 
 constexpr int kMaxRequeues = 3;
+// defaults: bitcoin/server.py REF_RATE, MINER_DEPTH, COPIES, SLACK, SLACK_FRAC
+constexpr double kRefRate = 34.6e9;
+constexpr int kDefaultDepth = 3;
+constexpr int kDefaultCopies = 3;
+constexpr double kSlack = 0.1;
+constexpr double kSlackFrac = 0.25;
+
+// about one LSP epoch of one MI355X, to a power of two (server.py default_job_size)
+uint64_t default_job_size(double epoch_s) {
+    long b = std::lround(std::log2(std::max(1.0, kRefRate * epoch_s)));
+    return 1ull << std::min(40L, std::max(30L, b));
+}
 
 bool g_log = false;
 
@@ -63,9 +80,30 @@ uint64_t env_u64(const char* name, uint64_t dflt) {
     return (end && *end == '\0' && v > 0) ? (uint64_t)v : dflt;
 }
 
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// A range of one request.  The same Job sits in the queue of every miner holding a copy of
+// it (speculative copies); `done` once any copy answered (bitcoin/server.py Job).
 struct Job {
     uint64_t req, lo, hi;
-    int requeues = 0;
+    int requeues = 0;   // losses of a miner that was computing this job
+    double sent = 0.0;  // first dispatch
+    bool done = false;
+    std::map<long long, double> holders;  // miner -> when its copy was sent
+    double size() const { return (double)(hi - lo) + 1.0; }
+};
+using JobP = std::shared_ptr<Job>;
+
+// Work and time of a miner's recent jobs, halved at each new result (server.py MinerRate).
+struct MinerRate {
+    double work = 0.0, secs = 0.0;
+    void add(double n, double dt) {
+        work = 0.5 * work + n;
+        secs = 0.5 * secs + std::max(dt, 1e-6);
+    }
+    double rate() const { return work / secs; }
 };
 
 struct Request {
@@ -74,7 +112,7 @@ struct Request {
     std::string data;
     uint64_t next_lo, upper;
     bool cut_all = false;  // every nonce is in some job (next_lo cannot pass 2^64-1)
-    std::deque<Job> requeued;
+    std::deque<JobP> requeued;
     int inflight = 0;
     bool has_best = false;
     uint64_t bh = 0, bn = 0;
@@ -83,26 +121,37 @@ struct Request {
     // nonces not yet handed to a miner (up to 2^64: hence 128 bits)
     unsigned __int128 remaining() const {
         unsigned __int128 n = cut_all ? 0 : (unsigned __int128)upper - next_lo + 1;
-        for (const Job& j : requeued) n += (unsigned __int128)j.hi - j.lo + 1;
+        for (const JobP& j : requeued) n += (unsigned __int128)j->hi - j->lo + 1;
         return n;
     }
-    Job pop_job(uint64_t size) {
+    // a requeued job, else the next `size` nonces -- or all that is left when less than a
+    // quarter job would remain (server.py Request.pop_job)
+    JobP pop_job(uint64_t size) {
         if (!requeued.empty()) {
-            Job j = requeued.front();
+            JobP j = requeued.front();
             requeued.pop_front();
             return j;
         }
         const uint64_t lo = next_lo;
-        const uint64_t hi = upper - lo < size - 1 ? upper : lo + (size - 1);
+        const unsigned __int128 left = (unsigned __int128)upper - lo + 1;
+        const uint64_t hi = left < (unsigned __int128)size + size / 4 ? upper : lo + (size - 1);
         if (hi == upper) cut_all = true;
         else next_lo = hi + 1;
-        return Job{id, lo, hi, 0};
+        auto j = std::make_shared<Job>();
+        j->req = id;
+        j->lo = lo;
+        j->hi = hi;
+        return j;
     }
 };
 
+// bitcoin/server.py's Scheduler: depth, speculative copies (hedge "overdue"), the requeue
+// cap charged to the job a lost miner was computing.
 class Scheduler {
    public:
-    Scheduler(uint64_t job_size, int depth) : job_size_(job_size), depth_(depth < 1 ? 1 : depth) {}
+    Scheduler(uint64_t job_size, int depth, int copies, double slack, double slack_frac)
+        : job_size_(job_size), depth_(depth < 1 ? 1 : depth), copies_(copies < 1 ? 1 : copies),
+          slack_(slack), slack_frac_(slack_frac) {}
 
     std::deque<long long> abandoned;  // clients to disconnect
 
@@ -144,7 +193,7 @@ class Scheduler {
     }
 
     // (miner, job, data) of the next dispatch; false when none
-    bool next_assignment(long long& miner, Job& job, std::string& data) {
+    bool next_assignment(long long& miner, JobP& job, std::string& data) {
         long long best_m = 0;
         bool found = false;
         for (auto& [m, q] : miners_) {
@@ -164,8 +213,10 @@ class Scheduler {
                 (x.inflight == r->inflight && x.remaining() < r->remaining()))
                 r = &x;
         }
-        if (!r) return false;
+        if (!r) return speculate(miner, job, data);
         job = r->pop_job(job_size_);
+        job->sent = now_s();
+        job->holders[best_m] = job->sent;
         r->inflight++;
         miners_[best_m].push_back(job);
         turn_[best_m] = tick_++;
@@ -174,13 +225,43 @@ class Scheduler {
         return true;
     }
 
+    // when next_assignment() may hand out a copy without any message arriving (< 0: never)
+    double next_wakeup() {
+        if (copies_ <= 1) return -1.0;
+        bool idle = false;
+        for (auto& [m, q] : miners_) idle = idle || q.empty();
+        if (!idle) return -1.0;
+        for (auto& [id, r] : requests_)
+            if (r.has_pending()) return -1.0;
+        double best = -1.0;
+        for (const JobP& j : unfinished()) {
+            if ((int)j->holders.size() >= copies_) continue;
+            const double t = overdue_at(*j);
+            if (t >= 0.0 && (best < 0.0 || t < best)) best = t;
+        }
+        return best;
+    }
+
     // folds a miner's Result (its oldest job); true with the client and answer when done
     bool result(long long miner, uint64_t h, uint64_t n, long long& client, uint64_t& bh, uint64_t& bn) {
         auto it = miners_.find(miner);
         if (it == miners_.end() || it->second.empty()) return false;
-        Job job = it->second.front();
+        JobP job = it->second.front();
         it->second.pop_front();
-        auto r = requests_.find(job.req);
+        const double now = now_s();
+        double sent = job->sent;
+        auto hs = job->holders.find(miner);
+        if (hs != job->holders.end()) {
+            sent = hs->second;
+            job->holders.erase(hs);
+        }
+        auto d = done_at_.find(miner);
+        const double start = std::max(sent, d == done_at_.end() ? sent : d->second);
+        done_at_[miner] = now;
+        rates_[miner].add(job->size(), now - start);
+        if (job->done) return false;  // another copy answered first
+        job->done = true;
+        auto r = requests_.find(job->req);
         if (r == requests_.end()) return false;  // the client is gone: ignore the result
         Request& q = r->second;
         q.inflight--;
@@ -197,18 +278,25 @@ class Scheduler {
         return true;
     }
 
+    // a lost miner's unfinished jobs go back to the front of their requests' queues unless
+    // another miner holds a copy; only the job it was computing (its oldest) is charged
+    // toward the requeue cap (server.py Scheduler.lost)
     void lost(long long conn) {
         auto it = miners_.find(conn);
         if (it != miners_.end()) {
-            std::deque<Job> jobs = std::move(it->second);
+            std::deque<JobP> jobs = std::move(it->second);
             miners_.erase(it);
             turn_.erase(conn);
+            rates_.erase(conn);
+            done_at_.erase(conn);
             logf("miner %lld lost", conn);
-            for (auto j = jobs.rbegin(); j != jobs.rend(); ++j) {  // oldest ends up first
+            const JobP current = jobs.empty() ? nullptr : jobs.front();
+            for (auto jt = jobs.rbegin(); jt != jobs.rend(); ++jt) {  // oldest ends up first
+                const JobP& j = *jt;
+                j->holders.erase(conn);
                 auto r = requests_.find(j->req);
-                if (r == requests_.end()) continue;
-                r->second.inflight--;
-                if (++j->requeues > kMaxRequeues) {
+                if (j->done || r == requests_.end()) continue;
+                if (j == current && ++j->requeues > kMaxRequeues) {
                     logf("job [%llu, %llu] lost %d miners: request %llu abandoned, client %lld disconnected",
                          (unsigned long long)j->lo, (unsigned long long)j->hi, j->requeues,
                          (unsigned long long)j->req, r->second.client);
@@ -216,7 +304,13 @@ class Scheduler {
                     requests_.erase(r);
                     continue;
                 }
-                r->second.requeued.push_front(*j);
+                if (!j->holders.empty()) {
+                    logf("job [%llu, %llu] of request %llu still held by %zu miner(s)", (unsigned long long)j->lo,
+                         (unsigned long long)j->hi, (unsigned long long)j->req, j->holders.size());
+                    continue;
+                }
+                r->second.inflight--;
+                r->second.requeued.push_front(j);
                 logf("job [%llu, %llu] of request %llu requeued", (unsigned long long)j->lo,
                      (unsigned long long)j->hi, (unsigned long long)j->req);
             }
@@ -231,13 +325,107 @@ class Scheduler {
         }
     }
 
+    long long speculated() const { return speculated_; }
+
    private:
     uint64_t job_size_;
-    int depth_;
+    int depth_, copies_;
+    double slack_, slack_frac_;
     uint64_t next_id_ = 1, tick_ = 0;
+    long long speculated_ = 0;
     std::map<uint64_t, Request> requests_;
-    std::map<long long, std::deque<Job>> miners_;
+    std::map<long long, std::deque<JobP>> miners_;
     std::map<long long, uint64_t> turn_;
+    std::map<long long, MinerRate> rates_;
+    std::map<long long, double> done_at_;
+
+    // a miner's learned rate, a new miner's the median of the known ones (< 0: none known)
+    double rate(long long miner) const {
+        auto it = rates_.find(miner);
+        if (it != rates_.end()) return it->second.rate();
+        std::vector<double> known;
+        for (auto& [m, r] : rates_) known.push_back(r.rate());
+        if (known.empty()) return -1.0;
+        std::sort(known.begin(), known.end());
+        return known[known.size() / 2];
+    }
+
+    // when `miner`'s Result for `job` is due plus the slack (< 0: unknown)
+    double expected(const Job& job, long long miner) const {
+        const double rt = rate(miner);
+        if (rt <= 0.0) return -1.0;
+        auto d = done_at_.find(miner);
+        double t = d == done_at_.end() ? 0.0 : d->second;
+        auto q = miners_.find(miner);
+        if (q == miners_.end()) return -1.0;
+        for (const JobP& j : q->second) {
+            auto h = j->holders.find(miner);
+            t = std::max(t, h == j->holders.end() ? j->sent : h->second) + j->size() / rt;
+            if (j.get() == &job) return t + std::max(slack_, slack_frac_ * j->size() / rt);
+        }
+        return -1.0;
+    }
+
+    // when every copy of `job` is overdue (< 0: some holder's rate is unknown)
+    double overdue_at(const Job& job) const {
+        double worst = -1.0;
+        for (auto& [m, sent] : job.holders) {
+            const double t = expected(job, m);
+            if (t < 0.0) return -1.0;
+            worst = std::max(worst, t);
+        }
+        return worst;
+    }
+
+    std::vector<JobP> unfinished() const {
+        std::vector<JobP> out;
+        for (auto& [m, q] : miners_)
+            for (const JobP& j : q)
+                if (!j->done && requests_.count(j->req) && std::find(out.begin(), out.end(), j) == out.end())
+                    out.push_back(j);
+        return out;
+    }
+
+    bool speculate(long long& miner, JobP& job, std::string& data) {
+        if (copies_ <= 1) return false;
+        long long idle = 0;
+        bool any = false;
+        double idle_rate = 0.0;
+        for (auto& [m, q] : miners_) {
+            if (!q.empty()) continue;
+            const double rt = std::max(0.0, rate(m));
+            if (!any || rt > idle_rate || (rt == idle_rate && turn_.at(m) < turn_.at(idle))) {
+                idle = m;
+                idle_rate = rt;
+                any = true;
+            }
+        }
+        if (!any) return false;
+        const double now = now_s();
+        JobP best;
+        double best_t = 0.0;
+        for (const JobP& j : unfinished()) {
+            if ((int)j->holders.size() >= copies_) continue;
+            const double t = overdue_at(*j);
+            if (t < 0.0 || t > now) continue;
+            if (!best || t < best_t || (t == best_t && j->sent < best->sent)) {
+                best = j;
+                best_t = t;
+            }
+        }
+        if (!best) return false;
+        logf("copy of job [%llu, %llu] of request %llu to miner %lld (held by %zu miner(s), overdue)",
+             (unsigned long long)best->lo, (unsigned long long)best->hi, (unsigned long long)best->req, idle,
+             best->holders.size());
+        best->holders[idle] = now;
+        miners_[idle].push_back(best);
+        turn_[idle] = tick_++;
+        speculated_++;
+        miner = idle;
+        job = best;
+        data = requests_.at(best->req).data;
+        return true;
+    }
 };
 
 }  // namespace
@@ -254,7 +442,11 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "server: cannot listen on port %s\n", argv[1]);
         return 1;
     }
-    Scheduler sched(env_u64("GPUHASH_JOB_SIZE", 1ull << 34), (int)env_u64("GPUHASH_MINER_DEPTH", 1));
+    const char* backup = std::getenv("GPUHASH_BACKUP");
+    const int copies = backup && std::strcmp(backup, "0") == 0 ? 1 : (int)env_u64("GPUHASH_COPIES", kDefaultCopies);
+    Scheduler sched(env_u64("GPUHASH_JOB_SIZE", default_job_size(params.epoch_ms / 1000.0)),
+                    (int)env_u64("GPUHASH_MINER_DEPTH", kDefaultDepth),
+                    copies, kSlack, kSlackFrac);
 
     auto dispatch = [&] {
         while (!sched.abandoned.empty()) {
@@ -262,14 +454,14 @@ int main(int argc, char** argv) {
             sched.abandoned.pop_front();
         }
         long long miner;
-        Job job;
+        JobP job;
         std::string data;
         while (sched.next_assignment(miner, job, data)) {
             BtcMsg req;
             req.type = lspn::Request;
             req.data = data;
-            req.lower = job.lo;
-            req.upper = job.hi;
+            req.lower = job->lo;
+            req.upper = job->hi;
             if (!srv.write(miner, lspn::btc_marshal(req))) {
                 sched.lost(miner);
                 while (!sched.abandoned.empty()) {
@@ -281,7 +473,13 @@ int main(int argc, char** argv) {
     };
 
     for (;;) {
-        lspn::Server::Event e = srv.read();
+        // wake for the scheduler's own timer (the next job to become overdue) as for a message
+        const double wake = sched.next_wakeup();
+        lspn::Server::Event e = wake < 0.0 ? srv.read() : srv.read_until(wake);
+        if (e.timed_out) {
+            dispatch();
+            continue;
+        }
         if (e.lost) {
             logf("connection %lld %s", e.conn, e.reason == "closed" ? "closed" : ("lost (" + e.reason + ")").c_str());
             sched.lost(e.conn);

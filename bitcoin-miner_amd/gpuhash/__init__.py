@@ -91,6 +91,15 @@ class Stats(ctypes.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
+def compressions_per_nonce(rec: dict) -> int:
+    """SHA-256 compressions one nonce of a launch costs: its `c` nonce-bearing blocks, plus
+    the all-constant padding block an EX layout compresses from a per-nonce state (message
+    lengths 44-53 mod 64 at 10-12 digits).  The roofline charges
+    OPS_PER_BLOCK per compression; SURVEY 8(d)'s c-based figure
+    undercounts an EX launch's work by half."""
+    return int(rec["c"]) + (1 if rec["EX"] else 0)
+
+
 class LaunchRecord(ctypes.Structure):
     """gpuhash_launch_record (include/gpuhash.h)."""
     _fields_ = [(n, ctypes.c_int32) for n in ("device", "J", "C2", "EX", "digits", "c", "shard",

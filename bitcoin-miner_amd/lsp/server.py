@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import queue
 import threading
+import time
 
 import lspnet
 
@@ -39,7 +40,19 @@ class Server:
     def Read(self) -> tuple[int, bytes]:
         """Blocks for (connID, payload) from any client.  Raises LSPError(conn_id) when a
         client's connection is lost or closed (conn_id 0 once the server is closed)."""
-        item = self._reads.get()
+        return self.read_until(None)
+
+    def read_until(self, deadline: float | None):
+        """Read(), but returns None once time.monotonic() passes `deadline` with nothing
+        to return (None: block like Read).  Not in server_api.go: the bitcoin server uses
+        it to wake for its own timers (speculative job copies) between messages."""
+        try:
+            if deadline is None:
+                item = self._reads.get()
+            else:
+                item = self._reads.get(timeout=max(0.0, deadline - time.monotonic()))
+        except queue.Empty:
+            return None
         if item[0] == "data":
             return item[1], item[2]
         if item[0] == "closed":
@@ -96,7 +109,7 @@ class Server:
                 self._conns[cid] = ConnState(cid, self._p.WindowSize, self._p.EpochLimit, self._sender(addr))
             st = self._conns.get(cid)
             if st is not None:
-                st.silent = 0
+                st.mark_heard()
                 self._conn.write_to(NewAck(cid, 0).marshal(), addr)
             return
         st = self._conns.get(m.ConnID)

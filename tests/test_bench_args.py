@@ -78,6 +78,23 @@ def test_roofline_of_the_dominant_kernel(monkeypatch):
     assert r["target_frac"] == 0.70 and r["target_met"] is (r["frac"] >= 0.70)
 
 
+def test_roofline_charges_an_extra_block_layout_two_compressions(monkeypatch):
+    """an EX launch (message length 44-53 mod 64 at 10-12 digits) has
+    c = 1 nonce-bearing block but compresses the constant padding block per nonce too."""
+    monkeypatch.setattr(bench, "pmc_source", lambda cfg, key, cycles=None: (None, {"used": False}))
+    recs = [_rec(0, 13, 1 << 30, 51.7, c=1, EX=1)]  # 20.77 GH/s (DESIGN 4.3)
+    r = bench.roofline("2", recs)
+    assert r["kernel"] == "k_scan<J=13,C2=0,EX=1,MODE=0>"
+    assert (r["compressions_per_nonce"], r["ops_per_nonce"], r["ops_per_nonce_c_based"]) == (
+        2, 2 * bench.OPS_PER_BLOCK, bench.OPS_PER_BLOCK)
+    want = (1 << 30) * 2 * bench.OPS_PER_BLOCK / 0.0517 / 1e12
+    assert r["achieved"] == pytest.approx(want, rel=1e-3)
+    assert 0.70 < r["frac"] < 0.75  # at the c-based count it read 0.36 (VERDICT r05 weak 2)
+    import gpuhash
+    assert gpuhash.compressions_per_nonce({"c": 2, "EX": 0}) == 2
+    assert gpuhash.compressions_per_nonce({"c": 1, "EX": 0}) == 1
+
+
 # ---- the 2^40 search leg (VERDICT r03 item 1) ----
 
 def _srec(shard, dev, lo, hi, ms, stream_dev=None, J=4):

@@ -157,7 +157,7 @@ def test_scheduler_drops_lost_client_and_ignores_late_results():
 def test_full_u64_request_cuts_jobs_lazily():
     # [0, 2^64-1] is 2^30 jobs of 2^34: the scheduler must not materialise them
     import time
-    s = bserver.Scheduler()
+    s = bserver.Scheduler(job_size=1 << 34)
     t = time.time()
     rid = s.add_request(client=100, data="a", lower=0, upper=(1 << 64) - 1)
     assert time.time() - t < 0.1

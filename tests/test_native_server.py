@@ -293,3 +293,61 @@ def test_jobs_must_fit_one_datagram_python_and_compiled(procs, plain_server, min
     assert s.request("d" * n, 99) == oracle.min(b"d" * n, 0, 99)
     log = s.log()
     assert "would not fit a 2000-byte LSP datagram" in log, log
+
+
+@pytest.mark.parametrize("which", ["python", "compiled"])
+def test_overdue_job_is_copied_to_an_idle_miner(procs, plain_server, miner_bin, oracle, which):
+    """Speculative copies (bitcoin/server.py Scheduler, csrc/server_main.cpp Scheduler): a
+    miner that answered once and then sits on its next job forever -- its LSP connection
+    alive, so the server never sees it lost -- does not hold that request up.  Once the
+    job is overdue by the miner's learned rate, an idle miner gets a copy and its Result
+    answers the client."""
+    import queue
+    if which == "compiled":
+        s = System(procs, plain_server, miner_bin, GPUHASH_JOB_SIZE=10 ** 6)
+        port, log = s.port, s.log
+    else:
+        lines = queue.Queue()
+        holder = {}
+        threading.Thread(target=bserver_serve, args=(P, 10 ** 6, holder, lines.put), daemon=True).start()
+        while "srv" not in holder:
+            time.sleep(0.01)
+        port = holder["srv"].port
+
+        def log():
+            out = []
+            while not lines.empty():
+                out.append(lines.get())
+            return "\n".join(out)
+
+    class Stuck:  # answers its first job, then never returns
+        calls = 0
+
+        def min(self, msg, lo, hi):
+            Stuck.calls += 1
+            if Stuck.calls > 1:
+                threading.Event().wait()
+            return oracle.min(msg.encode(), lo, hi)
+
+    threading.Thread(target=bminer.run, args=(f"127.0.0.1:{port}", Stuck(), P), daemon=True).start()
+    time.sleep(0.3)
+    hp = f"127.0.0.1:{port}"
+    assert bclient.request(hp, "first", 999, P) == oracle.min(b"first", 0, 999)  # the stuck miner learns a rate
+    if which == "compiled":
+        s.miner()
+    else:
+        class Eng:
+            def min(self, msg, lo, hi):
+                return oracle.min(msg.encode(), lo, hi)
+        threading.Thread(target=bminer.run, args=(hp, Eng(), P), daemon=True).start()
+    time.sleep(0.3)
+    t = time.time()
+    assert bclient.request(hp, "second", 999, P) == oracle.min(b"second", 0, 999)
+    assert time.time() - t < 5.0
+    assert Stuck.calls == 2  # the stuck miner took the job; a copy answered it
+    assert "copy of job [0, 999]" in log()
+
+
+def bserver_serve(params, job_size, holder, log):
+    from bitcoin import server as bserver
+    bserver.serve(0, params=params, job_size=job_size, ready=lambda srv: holder.setdefault("srv", srv), log=log)

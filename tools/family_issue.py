@@ -30,6 +30,8 @@ sys.path.insert(0, os.path.join(ROOT, "bitcoin-miner_amd"))
 
 CUS = 256
 LANES = 64
+OPS_PER_BLOCK = 1378                  # bench.py / SURVEY 8(d): one compression
+VALU_PEAK = CUS * 128 * 2.4e9         # bench.py VALU_PEAK_T, lane-ops/s
 
 # (family, message length, digits, policy, log2 nonces)
 CASES = [
@@ -72,11 +74,21 @@ def run(reps: int) -> None:
             r = recs[0]
             ms = statistics.median(x["ms"] for x in recs)
             sclk = statistics.median(x["sclk_mhz"] for x in recs)
+            ghs = (hi - lo + 1) / ms / 1e6
+            comp = gpuhash.compressions_per_nonce(r)
             print(json.dumps({"family": fam, "msg_len": m, "digits": d, "policy": pol,
                               "lower": lo, "upper": hi, "nonces": hi - lo + 1,
                               "variant": f"J={r['J']},C2={r['C2']},EX={r['EX']}",
                               "kernel_ms": round(ms, 3), "sclk_mhz": round(sclk, 1),
-                              "GHs": round((hi - lo + 1) / ms / 1e6, 3), "result": list(res)}),
+                              "GHs": round(ghs, 3),
+                              # algorithmic ops: OPS_PER_BLOCK per compression (c + EX), with
+                              # SURVEY 8(d)'s c-based count beside it
+                              "compressions_per_nonce": comp,
+                              "ops_per_nonce": OPS_PER_BLOCK * comp,
+                              "ops_per_nonce_c_based": OPS_PER_BLOCK * r["c"],
+                              "frac": round(ghs * 1e9 * OPS_PER_BLOCK * comp / VALU_PEAK, 4),
+                              "frac_c_based": round(ghs * 1e9 * OPS_PER_BLOCK * r["c"] / VALU_PEAK, 4),
+                              "result": list(res)}),
                   flush=True)
 
 

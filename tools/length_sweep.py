@@ -25,6 +25,13 @@ with gpuhash.Engine([0]) as e:
             dt = time.perf_counter() - t
             recs = e.launches()
             top = max(recs, key=lambda r: r["nonces"])
+            kms = sum(r["ms"] for r in recs)
+            ops = sum(r["nonces"] * 1378 * gpuhash.compressions_per_nonce(r) for r in recs)
             print(json.dumps({"msg_len": m, "digits": d, "GHs": round(N / dt / 1e9, 3),
+                              "kernel_GHs": round(N / kms / 1e6, 3),
                               "variants": sorted({(r["J"], r["C2"], r["EX"]) for r in recs}),
+                              "compressions_per_nonce": round(ops / 1378 / N, 3),
+                              # algorithmic ops (1,378 per compression, c + EX) over the kernels'
+                              # HIP-event time, against the 78.6 T VALU peak (bench.py)
+                              "frac": round(ops / (kms * 1e-3) / (256 * 128 * 2.4e9), 4),
                               "sclk_mhz": round(top["sclk_mhz"]), "result": list(res)}), flush=True)
