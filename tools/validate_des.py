@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""Checks the discrete-event model (tests/lsp_des.py) against real runs of the system:
+the same shape run K times through tools/system_bench.py -- real server, real LSP over
+UDP with lspnet's drops, real clients, and miners that are either the GPU miner (on the
+GPU box) or tools/emu_miner.py (a miner that sleeps n / rate: CPU only) -- and N seeds of
+the model, per server policy.  Prints one JSON line per policy with both distributions.
+
+  python tools/validate_des.py --emulate --runs 24 --parallel 6     # CPU, here
+  python tools/validate_des.py --runs 8                              # GPU box: one miner, real GPU
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "bitcoin-miner_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+GPU = 34.6e9
+POLICIES = {
+    # name: (system_bench args, Scheduler kwargs for the model)
+    "round5": (["--job-bits", "34", "--depth", "1", "--copies", "1"], dict(job_size=1 << 34, depth=1)),
+    "defaults": ([], None),  # bitcoin.server.make_scheduler(epoch_s=2.0)
+}
+
+
+def stats(xs: list[float]) -> dict:
+    xs = sorted(xs)
+    return {"n": len(xs), "mean": round(statistics.mean(xs), 3), "median": round(xs[len(xs) // 2], 3),
+            "p90": round(xs[min(len(xs) - 1, int(0.9 * len(xs)))], 3), "min": round(xs[0], 3),
+            "max": round(xs[-1], 3)}
+
+
+def real_run(args, extra: list[str], k: int) -> dict:
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "system_bench.py"), "--clients", str(args.clients),
+           "--bits", str(args.bits), "--miners", "1", "--kill-after", "-1", "--label", f"run {k}"] + extra
+    if args.emulate:
+        cmd += ["--emulate", str(GPU)]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    if out.returncode != 0:
+        raise RuntimeError(out.stderr[-2000:])
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def model(policy, seeds: int, clients: int, bits: int, client_start: float) -> list[dict]:
+    import lsp
+    import lsp_des
+    from bitcoin import server as bserver
+    reqs = [(f"client-{i:02d}", 0, 1 << bits) for i in range(clients)]
+    out = []
+    for s in range(seeds):
+        sch = bserver.make_scheduler(epoch_s=2.0) if policy is None else bserver.Scheduler(**policy)
+        out.append(lsp_des.run_system(sch, [GPU], 1, reqs, params=lsp.NewParams(), drop=0.10, seed=s,
+                                      client_start=client_start))
+    return out
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--runs", type=int, default=8)
+    ap.add_argument("--seeds", type=int, default=400)
+    ap.add_argument("--parallel", type=int, default=1)
+    ap.add_argument("--emulate", action="store_true")
+    ap.add_argument("--clients", type=int, default=4)
+    ap.add_argument("--bits", type=int, default=35)
+    ap.add_argument("--policies", default="round5,defaults")
+    ap.add_argument("--out", default=None, help="also append each real run's line here")
+    args = ap.parse_args()
+    for name in args.policies.split(","):
+        extra, kw = POLICIES[name]
+        with cf.ThreadPoolExecutor(args.parallel) as ex:
+            runs = list(ex.map(lambda k: real_run(args, extra, k), range(args.runs)))
+        if args.out:
+            with open(args.out, "a") as f:
+                for r in runs:
+                    f.write(json.dumps(dict(r, policy=name)) + "\n")
+        # system_bench.py starts the clients 1.5 s (emulated) or 5 s (GPU) after the miners
+        sims = model(kw, args.seeds, args.clients, args.bits, 1.5 if args.emulate else 5.0)
+        work = args.clients * ((1 << args.bits) + 1)
+        print(json.dumps({
+            "policy": name, "miners": "emulated (sleep n/34.6e9)" if args.emulate else "GPU",
+            "shape": f"1 miner, {args.clients} clients x [0, 2^{args.bits}], 2 s epochs, limit 5, 10% drops",
+            "real_makespan_s": stats([r["wall_s"] for r in runs]),
+            "model_makespan_s": stats([s["makespan"] for s in sims]),
+            "real_busy_frac_wall": stats([r["busy_frac_wall"] for r in runs]),
+            "model_busy_frac_wall": stats([work / GPU / s["makespan"] for s in sims]),
+            "real_busy_frac_avail": stats([r["busy_frac_avail"] or 0.0 for r in runs]),
+            "model_busy_frac_avail": stats([s["busy_avail"] for s in sims]),
+            "real_all_verified": all(r["all_results_verified"] in (True, None) for r in runs),
+        }), flush=True)
+
+
+if __name__ == "__main__":
+    main()
