@@ -542,15 +542,18 @@ def alone_rerun(make_engine, row: dict, t_all: float, barrier) -> dict:
     ranks wait at a barrier for this one), like rank 0's in-process repeat."""
     launches = []
     try:
-        eng = make_engine()
-        barrier()
-        t0 = time.perf_counter()
-        for lo, hi in row["windows"]:
-            eng.min(MSG, lo, hi)
-            launches += eng.launches()
-        barrier()
-        t_alone = time.perf_counter() - t0
-        eng.close()
+        with make_engine() as eng:  # closed even when a call raises (ADVICE r05)
+            # a fresh context's first call reserves its buffers and events: one small search
+            # before the clock starts, so t_alone is hashing, as the N-device time is
+            lo0, hi0 = row["windows"][0]
+            eng.min(MSG, lo0, min(hi0, lo0 + (1 << 20)))
+            barrier()
+            t0 = time.perf_counter()
+            for lo, hi in row["windows"]:
+                eng.min(MSG, lo, hi)
+                launches += eng.launches()
+            barrier()
+            t_alone = time.perf_counter() - t0
     except Exception as e:  # noqa: BLE001 -- see above
         return {"shard": row["shard"], "device": row["device"], "windows": row["windows"],
                 "error": f"{type(e).__name__}: {e}"}
@@ -558,6 +561,30 @@ def alone_rerun(make_engine, row: dict, t_all: float, barrier) -> dict:
             "t_alone_s": round(t_alone, 3), "t_all_s": round(t_all, 3),
             "scaling_efficiency": round(t_alone / t_all, 4) if t_all > 0 else None,
             "alone_sclk_mhz": shard_rows(launches)[0]["sclk_mhz"] if launches else None}
+
+
+def distinct_gpu_summary(out: dict) -> str | None:
+    """One stderr line for a run over two or more distinct physical GPUs (VERDICT r05 item
+    5), so the tail of the driver's 8-GPU log reads on its own: per GPU of the search (else
+    of the timed steps) its kernel GH/s, in-kernel clock and (host,) PCI id, then the run's
+    scaling_efficiency.  None when the run had one physical GPU (rehearsals on one GPU)."""
+    for key in ("search_2p40", "search_2p40_inproc"):
+        s = out.get(key)
+        if s and s.get("shards"):
+            rows, what = s["shards"], key
+            break
+    else:
+        rows, what = out.get("shards") or [], "timed steps"
+    ids = [(r.get("host"), r.get("pci")) if r.get("pci") else (None, f"ordinal {r['device']}") for r in rows]
+    if len(set(ids)) < 2:
+        return None
+    parts = []
+    for r, (host, pci) in zip(rows, ids):
+        where = f"{host}/{pci}" if host else pci
+        parts.append(f"gpu {r['device']} [{where}] {r.get('kernel_GHs')} GH/s @ {r.get('sclk_mhz')} MHz")
+    eff = ((out.get("search_2p40") or {}).get("scaling") or {}).get("scaling_efficiency")
+    return (f"bench.py: {len(set(ids))} distinct GPUs ({what}): " + "; ".join(parts)
+            + f"; scaling_efficiency {eff}")
 
 
 def search_exit(out: dict, problems: list[str]) -> None:
@@ -669,6 +696,9 @@ def main_inproc(args, devs: list[int]) -> None:
     if n == 1:
         add_cpu_baselines(out, args)
     emit(out)
+    summary = distinct_gpu_summary(out)
+    if summary:
+        print(summary, file=sys.stderr, flush=True)
     eng.close()
     search_exit(out, problems)
 
@@ -848,6 +878,9 @@ def main_ranks(args, world: int, rank: int, local: int) -> None:
         if world == 1:
             add_cpu_baselines(out, args)
         emit(out)
+        summary = distinct_gpu_summary(out)
+        if summary:
+            print(summary, file=sys.stderr, flush=True)
     eng.close()
     dist.destroy_process_group()
     if rank == 0:

@@ -456,13 +456,26 @@ int gpuhash_device_count(void) {
     return count;
 }
 
+static bool valid_policy(int policy) {
+    const int base = policy & 15, flags = policy & ~15;
+    return base >= GPUHASH_LAYOUT_AUTO && base <= GPUHASH_LAYOUT_LANETABLE &&
+           !(flags & ~(GPUHASH_LAYOUT_TAIL_ALWAYS | GPUHASH_LAYOUT_TAIL_NEVER)) &&
+           flags != (GPUHASH_LAYOUT_TAIL_ALWAYS | GPUHASH_LAYOUT_TAIL_NEVER);
+}
+
 int gpuhash_shard_range(size_t msg_len, uint64_t lower, uint64_t upper, int nshards,
                         uint64_t* out_lower, uint64_t* out_upper) {
-    if (nshards < 1 || !out_lower || !out_upper || lower > upper) return GPUHASH_EINVAL;
+    return gpuhash_shard_range_policy(msg_len, lower, upper, nshards, GPUHASH_LAYOUT_AUTO, out_lower, out_upper);
+}
+
+int gpuhash_shard_range_policy(size_t msg_len, uint64_t lower, uint64_t upper, int nshards, int policy,
+                               uint64_t* out_lower, uint64_t* out_upper) {
+    if (nshards < 1 || !out_lower || !out_upper || lower > upper || !valid_policy(policy)) return GPUHASH_EINVAL;
     if (msg_len > GPUHASH_MAX_MSG) return GPUHASH_ETOOLONG;
     try {
-        // the same cost model and cut points as gpuhash_min's in-process shards
-        const std::vector<Shard> sh = shard_range(msg_len, lower, upper, nshards);
+        // the same cost model and cut points as gpuhash_min's in-process shards under the
+        // same layout policy (the cuts depend on it)
+        const std::vector<Shard> sh = shard_range(msg_len, lower, upper, nshards, policy);
         int used = 0;
         for (int k = 0; k < nshards; k++) {
             const Shard& s = sh[(size_t)k];
@@ -479,11 +492,7 @@ int gpuhash_shard_range(size_t msg_len, uint64_t lower, uint64_t upper, int nsha
 }
 
 int gpuhash_set_layout_policy(gpuhash_ctx* ctx, int policy) {
-    const int base = policy & 15, flags = policy & ~15;
-    if (!ctx || base < GPUHASH_LAYOUT_AUTO || base > GPUHASH_LAYOUT_LANETABLE ||
-        (flags & ~(GPUHASH_LAYOUT_TAIL_ALWAYS | GPUHASH_LAYOUT_TAIL_NEVER)) ||
-        flags == (GPUHASH_LAYOUT_TAIL_ALWAYS | GPUHASH_LAYOUT_TAIL_NEVER))
-        return GPUHASH_EINVAL;
+    if (!ctx || !valid_policy(policy)) return GPUHASH_EINVAL;
     std::lock_guard<std::mutex> lock(ctx->mu);
     ctx->policy = policy;
     return GPUHASH_OK;

@@ -56,29 +56,41 @@ struct JVal {
     enum Kind { Null, Bool, Num, Str, Composite } kind = Null;  // Composite: object or array
     std::string text;  // Str: the decoded UTF-8 bytes; Num: the literal
     bool b = false;
+    bool array = false;        // Composite: an array, whose elements are in `elems`
+    std::vector<JVal> elems;   // (a []byte field accepts an array of uint8)
 };
 
 // The members of one JSON object in document order (duplicates kept).
 using JObj = std::vector<std::pair<std::string, JVal>>;
 
-// Calls f(value) for every member whose key equals struct field `name` ignoring ASCII
-// case, in document order, stopping at the first f that returns false.  Go's
-// json.Unmarshal decodes EVERY such member into the field in order: a null member leaves
-// the field as an earlier one set it, and a member of the wrong type fails the message
-// even if a later member is fine (it keeps the first UnmarshalTypeError).
+// True if UTF-8 key `k` equals the ASCII struct field name `name` as encoding/json
+// matches them: ignoring ASCII case, with the two non-ASCII runes whose simple case
+// folding reaches an ASCII letter, the long s U+017F (~ s) and the Kelvin sign U+212A
+// (~ k) (fold.go equalFoldRight; gojson._FOLD).
+inline bool key_matches(const std::string& k, const char* name) {
+    size_t i = 0;
+    for (const char* p = name; *p; p++) {
+        if (i >= k.size()) return false;
+        char a;
+        if (k.compare(i, 2, "\xC5\xBF") == 0) { a = 's'; i += 2; }
+        else if (k.compare(i, 3, "\xE2\x84\xAA") == 0) { a = 'k'; i += 3; }
+        else { a = k[i++]; if (a >= 'A' && a <= 'Z') a = (char)(a - 'A' + 'a'); }
+        char b = *p;
+        if (b >= 'A' && b <= 'Z') b = (char)(b - 'A' + 'a');
+        if (a != b) return false;
+    }
+    return i == k.size();
+}
+
+// Calls f(value) for every member whose key matches struct field `name` (key_matches), in
+// document order, stopping at the first f that returns false.  Go's json.Unmarshal decodes
+// EVERY such member into the field in order: a null member leaves the field as an earlier
+// one set it, and a member of the wrong type fails the message even if a later member is
+// fine (it keeps the first UnmarshalTypeError).
 template <class F>
 inline bool jfields(const JObj& o, const char* name, F&& f) {
-    const size_t n = std::strlen(name);
     for (const auto& kv : o) {
-        if (kv.first.size() != n) continue;
-        bool eq = true;
-        for (size_t i = 0; i < n && eq; i++) {
-            char a = kv.first[i], b = name[i];
-            if (a >= 'A' && a <= 'Z') a = (char)(a - 'A' + 'a');
-            if (b >= 'A' && b <= 'Z') b = (char)(b - 'A' + 'a');
-            eq = a == b;
-        }
-        if (eq && !f(kv.second)) return false;
+        if (key_matches(kv.first, name) && !f(kv.second)) return false;
     }
     return true;
 }
@@ -259,7 +271,7 @@ class JsonReader {
             v.text = s_.substr(b, i_ - b);
             return true;
         }
-        if (c == '{' || c == '[') { v.kind = JVal::Composite; return composite(); }
+        if (c == '{' || c == '[') { v.kind = JVal::Composite; return composite(&v); }
         return false;
     }
     bool digits() {  // [0-9]+
@@ -270,14 +282,17 @@ class JsonReader {
     // Skips one object or array (any nesting) with the full grammar -- keys, colons and
     // separators checked -- so a document Go's Unmarshal rejects ([1 2], {1:2}, {"a"},
     // [,,]) is rejected here too.  Depth is bounded by the 2000-byte datagram.
-    bool composite() {
+    // An array's elements are kept in `arr->elems` (a []byte field reads them).
+    bool composite(JVal* arr) {
         if (eat('[')) {
+            arr->array = true;
             ws();
             if (eat(']')) return true;
             for (;;) {
                 ws();
                 JVal x;
                 if (!value(x)) return false;
+                arr->elems.push_back(std::move(x));
                 ws();
                 if (eat(',')) continue;
                 return eat(']');
@@ -473,13 +488,32 @@ inline bool lsp_unmarshal(const std::string& raw, LspMsg& m) {
     if (!JsonReader(raw).object(o)) return false;
     if (!get_int(o, "Type", m.type) || !get_int(o, "ConnID", m.conn) || !get_int(o, "SeqNum", m.seq)) return false;
     // []byte: each string member is base64-decoded in order (an invalid one fails the
-    // message); null sets a slice back to nil, as encoding/json does
+    // message); null sets a slice back to nil, as encoding/json does; an
+    // array is its elements, each a uint8 literal in [0, 255] or null (0), anything else
+    // failing the message (lsp/message.py byte_array)
     m.has_payload = false;
     m.payload.clear();
     return jfields(o, "Payload", [&](const JVal& f) {
         if (f.kind == JVal::Null) {
             m.has_payload = false;
             m.payload.clear();
+            return true;
+        }
+        if (f.kind == JVal::Composite && f.array) {
+            std::string bytes;
+            for (const JVal& e : f.elems) {
+                if (e.kind == JVal::Null) { bytes += '\0'; continue; }
+                if (e.kind != JVal::Num || e.text.empty() || e.text.size() > 3) return false;
+                unsigned v = 0;
+                for (char c : e.text) {
+                    if (c < '0' || c > '9') return false;
+                    v = v * 10 + (unsigned)(c - '0');
+                }
+                if (v > 255) return false;
+                bytes += (char)v;
+            }
+            m.payload = std::move(bytes);
+            m.has_payload = true;
             return true;
         }
         if (f.kind != JVal::Str || !b64decode(f.text, m.payload)) return false;
@@ -749,30 +783,38 @@ void event_loop(int fd, int epoch_ms, std::mutex& mu, const bool& stop, LoopLate
         int timeout = now >= next ? 0 : (int)std::chrono::duration_cast<std::chrono::milliseconds>(next - now).count() + 1;
         pollfd pfd{fd, POLLIN, 0};
         poll(&pfd, 1, std::min(timeout, 50));
-        std::lock_guard<std::mutex> lk(mu);
-        const auto t = clk::now();
-        bool is_epoch = t >= next;
-        if (is_epoch) {
-            const long long ms = std::chrono::duration_cast<std::chrono::milliseconds>(t - next).count();
-            late.max_ms = std::max(late.max_ms, ms);
-            if (ms > epoch.count()) {
-                late.late_epochs++;
-                if (diag)
-                    std::fprintf(stderr, "%s[%d]: epoch fired %lld ms late (epoch %lld ms)\n", role, (int)getpid(), ms,
-                                 (long long)epoch.count());
-            }
-            if (diag) {  // every 5 s: the latest epoch of the window
-                win_max = std::max(win_max, ms);
-                if (t - win_start >= std::chrono::seconds(5)) {
-                    std::fprintf(stderr, "%s[%d]: window max lateness %lld ms, run max %lld ms, %lld epochs >1 late\n",
-                                 role, (int)getpid(), win_max, late.max_ms, late.late_epochs);
-                    win_max = 0;
-                    win_start = t;
+        // LSP_DIAG lines are formatted under the lock and written after it is released, so a
+        // stalled stderr reader cannot hold up the endpoint's heartbeats
+        char line[2][192];
+        int nlines = 0;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            const auto t = clk::now();
+            bool is_epoch = t >= next;
+            if (is_epoch) {
+                const long long ms = std::chrono::duration_cast<std::chrono::milliseconds>(t - next).count();
+                late.max_ms = std::max(late.max_ms, ms);
+                if (ms > epoch.count()) {
+                    late.late_epochs++;
+                    if (diag)
+                        std::snprintf(line[nlines++], sizeof line[0], "%s[%d]: epoch fired %lld ms late (epoch %lld ms)\n",
+                                      role, (int)getpid(), ms, (long long)epoch.count());
                 }
+                if (diag) {  // every 5 s: the latest epoch of the window
+                    win_max = std::max(win_max, ms);
+                    if (t - win_start >= std::chrono::seconds(5)) {
+                        std::snprintf(line[nlines++], sizeof line[0],
+                                      "%s[%d]: window max lateness %lld ms, run max %lld ms, %lld epochs >1 late\n",
+                                      role, (int)getpid(), win_max, late.max_ms, late.late_epochs);
+                        win_max = 0;
+                        win_start = t;
+                    }
+                }
+                next = t + epoch;
             }
-            next = t + epoch;
+            tick(is_epoch);
         }
-        tick(is_epoch);
+        for (int k = 0; k < nlines; k++) std::fputs(line[k], stderr);
     }
 }
 

@@ -2,7 +2,8 @@
 shared by bitcoin.unmarshal (bitcoin.Message, bitcoin/message.go:16-21) and
 lsp.Message.unmarshal (lsp/message.go:17-22), and restated in C++ by csrc/lsp_native.h:
 
-  go_object   json.loads object hook: keys select struct fields ignoring (ASCII) case, and
+  go_object   json.loads object hook: keys select struct fields ignoring case (ASCII, and
+              the long s / Kelvin sign that fold to s / k), and
               EVERY matching member is kept in document order (Go decodes each of them)
   field       the value Unmarshal leaves in a scalar field: members in order, null
               skipped, a wrong-typed member fails the message
@@ -19,7 +20,11 @@ import re
 UINT64_MAX = (1 << 64) - 1
 INT64_MIN, INT64_MAX = -(1 << 63), (1 << 63) - 1
 
-_FOLD = str.maketrans("ABCDEFGHIJKLMNOPQRSTUVWXYZ", "abcdefghijklmnopqrstuvwxyz")
+# key folding as encoding/json matches a key to a field name: ASCII case, plus the two
+# non-ASCII runes whose simple case folding reaches an ASCII letter, the long s U+017F (~ s)
+# and the Kelvin sign U+212A (~ k) (fold.go equalFoldRight)
+_FOLD = str.maketrans({**{chr(c): chr(c + 32) for c in range(ord("A"), ord("Z") + 1)},
+                       "\u017f": "s", "\u212a": "k"})
 
 
 class Members(list):

@@ -43,6 +43,7 @@ TAIL_MIN_SPAN = 1 << 33
 # Every symbol include/gpuhash.h declares (tests check the .so exports all of them).
 EXPORTED = [
     "gpuhash_open", "gpuhash_ndevices", "gpuhash_device_count", "gpuhash_shard_range",
+    "gpuhash_shard_range_policy",
     "gpuhash_set_layout_policy", "gpuhash_min", "gpuhash_min_ex",
     "gpuhash_hash_range", "gpuhash_hash_cpu", "gpuhash_last_stats", "gpuhash_last_launches",
     "gpuhash_close",
@@ -133,6 +134,9 @@ def _lib(path: str | None = None) -> ctypes.CDLL:
     lib.gpuhash_device_count.restype = ctypes.c_int
     lib.gpuhash_shard_range.argtypes = [sz, u64, u64, ctypes.c_int, ctypes.POINTER(u64), ctypes.POINTER(u64)]
     lib.gpuhash_shard_range.restype = ctypes.c_int
+    lib.gpuhash_shard_range_policy.argtypes = [sz, u64, u64, ctypes.c_int, ctypes.c_int,
+                                               ctypes.POINTER(u64), ctypes.POINTER(u64)]
+    lib.gpuhash_shard_range_policy.restype = ctypes.c_int
     lib.gpuhash_min.argtypes = [vp, u8p, sz, u64, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]
     lib.gpuhash_min.restype = ctypes.c_int
     lib.gpuhash_set_layout_policy.argtypes = [vp, ctypes.c_int]
@@ -173,16 +177,21 @@ def device_count() -> int:
     return int(_lib().gpuhash_device_count())
 
 
-def shard_range(msg_len: int, lower: int, upper: int, nshards: int) -> list[tuple[int, int] | None]:
-    """gpuhash_shard_range: the engine's cost-balanced contiguous partition of the
-    inclusive [lower, upper] into nshards pieces (None = empty shard).  Host-only."""
+def shard_range(msg_len: int, lower: int, upper: int, nshards: int,
+                policy: int | None = None) -> list[tuple[int, int] | None]:
+    """gpuhash_shard_range(_policy): the engine's cost-balanced contiguous partition of the
+    inclusive [lower, upper] into nshards pieces (None = empty shard), priced under the
+    layout `policy` (default AUTO) as gpuhash_min's own shards are.  Host-only."""
     _check_u64("lower", lower)
     _check_u64("upper", upper)
     if isinstance(nshards, bool) or not isinstance(nshards, int) or nshards < 1:
         raise ValueError(f"nshards={nshards!r} must be an int >= 1")
     lo = (ctypes.c_uint64 * nshards)()
     hi = (ctypes.c_uint64 * nshards)()
-    rc = _lib().gpuhash_shard_range(int(msg_len), lower, upper, nshards, lo, hi)
+    if policy is None:
+        rc = _lib().gpuhash_shard_range(int(msg_len), lower, upper, nshards, lo, hi)
+    else:
+        rc = _lib().gpuhash_shard_range_policy(int(msg_len), lower, upper, nshards, int(policy), lo, hi)
     if rc < 0:
         raise GpuHashError(rc, "gpuhash_shard_range")
     return [(int(a), int(b)) if a <= b else None for a, b in zip(lo, hi)]

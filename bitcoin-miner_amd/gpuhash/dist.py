@@ -22,20 +22,22 @@ from typing import Callable, Iterable
 U64_MAX = (1 << 64) - 1
 
 
-def split_range(lower: int, upper: int, world: int,
-                msg_len: int | None = None) -> list[tuple[int, int] | None]:
+def split_range(lower: int, upper: int, world: int, msg_len: int | None = None,
+                policy: int | None = None) -> list[tuple[int, int] | None]:
     """Contiguous shards of the inclusive range, in rank order; None for an empty shard.
 
     With msg_len, the shards are of equal estimated COST (for message
     lengths 45-54 the digit groups differ in SHA blocks per nonce, so equal counts would
     leave the 2-block ranks last): the cut points come from the C ABI,
     gpuhash_shard_range, so in-process devices and processes shard identically.  Without
-    it, equal counts (a search function that is not the engine, e.g. the oracle)."""
+    it, equal counts (a search function that is not the engine, e.g. the oracle).  `policy`:
+    the layout policy the ranks' engines run (gpuhash_shard_range_policy; default AUTO),
+    since the cost of a digit group depends on its layout."""
     if lower > upper:
         raise ValueError("lower > upper")
     if msg_len is not None:
         from gpuhash import shard_range
-        return shard_range(msg_len, lower, upper, world)
+        return shard_range(msg_len, lower, upper, world, policy)
     count = upper - lower + 1
     out: list[tuple[int, int] | None] = []
     start = lower

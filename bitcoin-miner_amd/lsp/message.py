@@ -28,6 +28,22 @@ def b64decode_go(s: str) -> bytes:
         raise ValueError(f"illegal base64 data: {e}") from None
 
 
+def byte_array(v: list) -> bytes:
+    """A JSON array into a []byte, as encoding/json decodes one (any slice accepts an
+    array; only Marshal insists on base64): each element a uint8, i.e. an integer literal
+    in [0, 255] (strconv.ParseUint: no sign, fraction or exponent); null leaves its element
+    0; anything else fails the message."""
+    out = bytearray()
+    for x in v:
+        if x is None:
+            out.append(0)
+        elif isinstance(x, gojson.IntLit) and not x.text.startswith("-") and x <= 255:
+            out.append(int(x))
+        else:
+            raise ValueError(f"json: cannot unmarshal {x!r} into Go struct field Message.Payload of type uint8")
+    return bytes(out)
+
+
 class MsgType(enum.IntEnum):
     MsgConnect = 0  # connection request from a client
     MsgData = 1     # data from a client or the server
@@ -53,7 +69,8 @@ class Message:
         matching member decodes in order, a wrong-typed member fails the message (ValueError),
         an absent field keeps its zero value (Type 0 = MsgConnect).  Type / ConnID / SeqNum
         are ints (integer literals only); Payload is a []byte: a string member is base64
-        (StdEncoding, padded, CR / LF ignored), and null resets it to nil.  A Type outside
+        (StdEncoding, padded, CR / LF ignored), an array is its bytes (byte_array), and null
+        resets it to nil.  A Type outside
         the three kinds is kept as a plain int (the endpoints then ignore the message)."""
         d = gojson.loads(raw)
         if not isinstance(d, dict):
@@ -65,6 +82,8 @@ class Message:
                 payload = None
             elif isinstance(v, str):
                 payload = b64decode_go(v)
+            elif isinstance(v, list):
+                payload = byte_array(v)
             else:
                 raise ValueError(f"json: cannot unmarshal {v!r} into Go struct field Message.Payload")
         return Message(MsgType(t) if t in MsgType._value2member_map_ else t, conn, seq, payload)

@@ -118,6 +118,14 @@ int gpuhash_device_count(void);
 int gpuhash_shard_range(size_t msg_len, uint64_t lower, uint64_t upper, int nshards,
                         uint64_t *out_lower, uint64_t *out_upper);
 
+/* gpuhash_shard_range under a layout policy (gpuhash_set_layout_policy's values): the
+ * cost of a digit group depends on the layout that runs it, so gpuhash_min's in-process
+ * cuts under a non-AUTO policy are these, and a host sharding over processes with that
+ * policy passes it here to cut the same way.  gpuhash_shard_range is this with
+ * GPUHASH_LAYOUT_AUTO.  GPUHASH_EINVAL also for an invalid policy.  Host-only. */
+int gpuhash_shard_range_policy(size_t msg_len, uint64_t lower, uint64_t upper, int nshards, int policy,
+                               uint64_t *out_lower, uint64_t *out_upper);
+
 /* Layout choice for a digit group whose digits straddle two SHA blocks with the loop word
  * at W_1 of the last block, i.e. 5-8 digits in the last block.  Let
  * q = the digits in block B's W_0/W_1 (RQ = 10^q nonces per block B-1 value), nb1 = the

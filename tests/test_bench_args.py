@@ -229,12 +229,48 @@ def test_alone_rerun_reports_scaling_efficiency():
         def close(self):
             self.closed = True
 
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *exc):
+            self.close()
+
     eng = Eng()
     row = {"shard": 0, "device": 0, "windows": [[0, 99], [200, 299]]}
-    s = bench.alone_rerun(lambda: eng, row, 0.2, lambda: None)
-    assert eng.calls == [(0, 99), (200, 299)] and eng.closed
-    assert s["t_alone_s"] >= 0.1 and s["scaling_efficiency"] == pytest.approx(s["t_alone_s"] / 0.2, rel=1e-2)
+    s = bench.alone_rerun(lambda: eng, row, 0.3, lambda: None)
+    # one untimed warm-up call on the fresh context, then the windows
+    assert eng.calls == [(0, 99), (0, 99), (200, 299)] and eng.closed
+    assert 0.1 <= s["t_alone_s"] < 0.15 and s["scaling_efficiency"] == pytest.approx(s["t_alone_s"] / 0.3, rel=1e-2)
     assert s["alone_sclk_mhz"] == 2400.0
+
+
+def test_alone_rerun_closes_the_engine_when_a_call_fails():
+    class Eng:
+        closed = False
+
+        def min(self, msg, lo, hi):
+            raise RuntimeError("device lost")
+
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *exc):
+            Eng.closed = True
+
+    s = bench.alone_rerun(Eng, {"shard": 0, "device": 0, "windows": [[0, 9]]}, 1.0, lambda: None)
+    assert s["error"] == "RuntimeError: device lost" and Eng.closed
+
+
+def test_distinct_gpu_summary():
+    rows = [{"device": 0, "pci": "0000:10:00", "host": "n1", "kernel_GHs": 34.6, "sclk_mhz": 2365.0},
+            {"device": 1, "pci": "0000:20:00", "host": "n1", "kernel_GHs": 34.5, "sclk_mhz": 2360.0}]
+    out = {"search_2p40": {"shards": rows, "scaling": {"scaling_efficiency": 0.991}}}
+    line = bench.distinct_gpu_summary(out)
+    assert line.startswith("bench.py: 2 distinct GPUs (search_2p40): gpu 0 [n1/0000:10:00] 34.6 GH/s @ 2365.0 MHz")
+    assert line.endswith("scaling_efficiency 0.991")
+    same = [dict(r, pci="0000:10:00", device=0) for r in rows]  # shards on one GPU: no line
+    assert bench.distinct_gpu_summary({"search_2p40": {"shards": same}}) is None
+    assert bench.distinct_gpu_summary({"shards": [{"device": 0}, {"device": 0}]}) is None
 
 
 def test_alone_rerun_records_a_failure_instead_of_raising():

@@ -95,15 +95,15 @@ def _worker(rank, world, port, ndev, share, q, pinned=False):
     torch.cuda.get_device_properties = props
     args = types.SimpleNamespace(gpus=world, steps=2, warmup=1, no_cpu_baseline=True, cpu_seconds=1.0,
                                  config="2", inproc=None, search=(0, 9999), no_search=False)
-    out = io.StringIO()
-    sys.stdout = out
+    out, err = io.StringIO(), io.StringIO()
+    sys.stdout, sys.stderr = out, err
     code = 0
     try:
         bench.main_ranks(args, world, rank, rank)
     except SystemExit as e:
         code = e.code
-    sys.stdout = sys.__stdout__
-    q.put((rank, code, out.getvalue()))
+    sys.stdout, sys.stderr = sys.__stdout__, sys.__stderr__
+    q.put((rank, code, out.getvalue(), err.getvalue()))
 
 
 def _run(ndev, share, pinned=False):
@@ -114,11 +114,12 @@ def _run(ndev, share, pinned=False):
     procs = [ctx.Process(target=_worker, args=(r, world, port, ndev, share, q, pinned)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict((r, (c, o)) for r, c, o in (q.get(timeout=120) for _ in range(world)))
+    res = dict((r, (c, o, e)) for r, c, o, e in (q.get(timeout=120) for _ in range(world)))
     for p in procs:
         p.join(timeout=30)
-    code, text = res[0]
+    code, text, err = res[0]
     line = json.loads([x for x in text.splitlines() if x.startswith("{")][-1])
+    _run.stderr = err
     return code, line
 
 
@@ -145,6 +146,11 @@ def test_two_ranks_on_two_gpus_search_leg_and_inproc_repeat():
     assert sc["t_all_s"] == s["seconds"] and sc["scaling_efficiency"] > 0
     # the timed step spans [0, 2^33): checked against config 2's N = 2 golden
     assert line["matches_golden"] is True and line["result_check"]["golden_names"] == ["cfg2_bradfitz_2gpu"]
+    # a run over distinct GPUs says so in one stderr line
+    summ = [x for x in _run.stderr.splitlines() if "distinct GPUs" in x]
+    assert len(summ) == 1, _run.stderr
+    assert "2 distinct GPUs (search_2p40)" in summ[0] and "0000:10:00" in summ[0] and "0000:20:00" in summ[0]
+    assert f"scaling_efficiency {sc['scaling_efficiency']}" in summ[0] and "MHz" in summ[0]
 
 
 def test_ranks_pinned_to_one_visible_gpu_each():
@@ -165,3 +171,4 @@ def test_shared_gpu_rehearsal_repeats_ordinal_zero():
     assert line["search_2p40"]["matches_golden"] is True
     assert line["search_2p40_inproc"]["devices"] == [0, 0]
     assert "device_check" not in line
+    assert "distinct GPUs" not in _run.stderr  # one physical GPU: no summary

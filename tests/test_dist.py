@@ -55,6 +55,24 @@ def test_cost_balanced_split_through_the_abi():
         gd.split_range(0, 1, 0, msg_len=8)
 
 
+def test_split_under_a_layout_policy():
+    """the cuts depend on the layout policy (a digit group's cost is its
+    layout's), so gpuhash_shard_range_policy cuts as gpuhash_min does under that policy;
+    AUTO is gpuhash_shard_range.  Over [0, 2^40) of 'bradfitz' the 12-digit groups run
+    tail-digit launches under AUTO and not under TAIL_NEVER, so the two cut differently."""
+    import gpuhash
+    lo, hi = 0, (1 << 40) - 1
+    auto = gd.split_range(lo, hi, 8, msg_len=8)
+    assert gd.split_range(lo, hi, 8, msg_len=8, policy=gpuhash.LAYOUT_AUTO) == auto
+    never = gd.split_range(lo, hi, 8, msg_len=8, policy=gpuhash.LAYOUT_TAIL_NEVER)
+    assert never != auto
+    for cuts in (auto, never):
+        assert cuts[0][0] == lo and cuts[-1][1] == hi
+        assert all(b[0] == a[1] + 1 for a, b in zip(cuts, cuts[1:]))
+    with pytest.raises(gpuhash.GpuHashError):
+        gpuhash.shard_range(8, 0, 10, 2, gpuhash.LAYOUT_TAIL_ALWAYS | gpuhash.LAYOUT_TAIL_NEVER)
+
+
 def test_weak_range():
     assert gd.weak_range(0, 1 << 32, 0) == (0, (1 << 32) - 1)
     assert gd.weak_range(0, 1 << 37, 7) == (7 << 37, (1 << 40) - 1)

@@ -97,6 +97,17 @@ def _python(doc):
     return (int(m.Type), m.Data.encode(), m.Lower, m.Upper)
 
 
+def test_unicode_key_folding_reaches_bitcoin_fields(probe):
+    """'Haſh' (U+017F) sets Hash in Go; the Kelvin sign folds to 'k' (no field has one)."""
+    doc = '{"Type":2,"Haſh":77,"Nonce":5}'.encode()
+    assert (bitcoin.unmarshal(doc).Hash, bitcoin.unmarshal(doc).Nonce) == (77, 5)
+    out = subprocess.run([probe], input=doc.hex() + "\n", capture_output=True, text=True, timeout=30,
+                         check=True).stdout.split()
+    assert (int(out[4]), int(out[5])) == (77, 5)
+    import gojson
+    assert "\u212aind".translate(gojson._FOLD) == "kind" and "\u017f".translate(gojson._FOLD) == "s"
+
+
 def test_python_reader_decodes_like_go():
     for doc, want in CASES:
         assert _python(doc) == want, doc
@@ -154,6 +165,29 @@ LSP_CASES = [
     (b'{"tYpE":2,"cOnNiD":5,"seqnum":6,"X":[1,{"y":null}]}', (2, 5, 6, None)),
     (b'[1,2]', None),
     (b'{"Type":1,"X":NaN}', None),
+    # []byte from an array: encoding/json decodes a JSON array into any slice,
+    # each element a uint8 (ParseUint, <= 255), null leaving its element 0
+    (b'{"Type":1,"Payload":[104,105]}', (1, 0, 0, b"hi")),
+    (b'{"Type":1,"Payload":[]}', (1, 0, 0, b"")),
+    (b'{"Type":1,"Payload":[104,null,105]}', (1, 0, 0, b"h\x00i")),
+    (b'{"Type":1,"Payload":[0,255]}', (1, 0, 0, b"\x00\xff")),
+    (b'{"Type":1,"Payload":[256]}', None),
+    (b'{"Type":1,"Payload":[-1]}', None),
+    (b'{"Type":1,"Payload":[1.0]}', None),
+    (b'{"Type":1,"Payload":[1e1]}', None),
+    (b'{"Type":1,"Payload":["a"]}', None),
+    (b'{"Type":1,"Payload":[[1]]}', None),
+    (b'{"Type":1,"Payload":[true]}', None),
+    (b'{"Type":1,"Payload":{"a":1}}', None),
+    (b'{"Type":1,"Payload":[104],"payload":"eW8="}', (1, 0, 0, b"yo")),
+    (b'{"Type":1,"Payload":"eW8=","payload":[104]}', (1, 0, 0, b"h")),
+    (b'{"Type":1,"Payload":[104],"payload":null}', (1, 0, 0, None)),
+    # key folding beyond ASCII: the long s U+017F matches 's' (ADVICE r05); other
+    # non-ASCII letters match nothing
+    (b'{"Type":2,"\xc5\xbfeqNum":6}', (2, 0, 6, None)),
+    (b'{"Type":2,"SEQNUM":5,"\xc5\xbfeqnum":6}', (2, 0, 6, None)),
+    (b'{"Type":2,"\xc5\xbfeqNum":"x"}', None),
+    (b'{"Type":2,"\xc4\xb1d":1,"Conn\xc4\xb0D":3}', (2, 0, 0, None)),
 ]
 
 
