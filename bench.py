@@ -172,7 +172,7 @@ def cpu_baseline_multicore(seconds: float = 5.0) -> dict:
 # committed rocprofv3 PMC summary per bench config (tools/summarize_prof.py): each was
 # collected on the same bench.py workload, so its per-launch counters match this run's
 # launches of the same kernel
-PMC_SUMMARY = {"2": "r05_pmc_summary.json", "3": "r05c3_pmc_summary.json", "4": "r05c4_pmc_summary.json"}
+PMC_SUMMARY = {"2": "r06_pmc_summary.json", "3": "r06c3_pmc_summary.json", "4": "r06c4_pmc_summary.json"}
 
 
 def pmc_source(config: str, key, launch_cycles: float | None = None) -> tuple[dict | None, dict]:

@@ -3,35 +3,42 @@ pp.13-15: split each client Request into jobs, farm them to miners, merge the Re
 answer the client.
 
 Job chunking: the reference leaves "a suitable maximum job size"
-open.  Default: fixed jobs of 2^34 nonces, ~0.5 s on one MI355X -- big enough that the
-per-job overhead (one LSP round trip + one gpuhash_min call, ~ms, plus an epoch-long
-stall whenever a message is dropped) stays small, small enough that a killed miner
-loses half a second of work and 16 concurrent requests spread over 8 miners
-(GPUHASH_JOB_SIZE overrides the size).
+open.  Default: fixed jobs of about one LSP epoch of one MI355X, a power of two --
+2^36 nonces at the reference's 2 s epochs (default_job_size).  Each job is a Request and
+a Result over a window-1 connection whose dropped messages wait for the next epoch, so
+jobs much shorter than an epoch leave the GPU waiting on the connection; a request's
+last sliver (under a quarter job) rides with the job before it.  GPUHASH_JOB_SIZE
+overrides the size.
+
+Depth and speculative copies: a miner holds up to MINER_DEPTH (3) jobs, so its next
+Request is already there while a Result or a Request waits for a resend; when nothing is
+left to hand out, a miner holding nothing takes a copy of a job that is overdue by its
+holder's learned rate (up to COPIES live copies, the first Result wins), which covers a
+dropped Result and a killed miner, which LSP reports only after EpochLimit silent epochs
+(10 s by default).  DESIGN.md 6.2-6.4 has the model (tests/lsp_des.py) and the
+measurements behind these defaults.
 
 Per-miner sizing (GPUHASH_JOB_SECONDS=t, or Scheduler(sizing=Sizing(...))): each job is
 sized for the miner that takes it, to last ~t.  A miner's rate is learned from its own
 results (work and wall time of its recent jobs, halved at every new result); its first
-job is a 2^22-nonce probe.  This serves miners of
-very different speeds (a CPU miner running the reference loop next to MI355X miners: a
-2^34 job on it takes minutes) and spreads the end of a lone big request over every
-miner (no job larger than its uncut remainder over its share of the miners, down to a
-quarter job).  It is not the default because with lossy links its jobs, shorter than
-fixed 2^34 ones whenever miners share a GPU, pay more resend stalls: BASELINE config 5
-as run on a 1-GPU box (8 miners on one GPU, 10% drops) measured 29.6-30.9 GH/s against
-33.2-33.7 with fixed jobs.
+job is a 2^22-nonce probe.  This serves miners of very different speeds (a CPU miner
+running the reference loop next to MI355X miners) and spreads the end of a lone big
+request over every miner.  It is not the default: on lossy links its shorter jobs pay
+more resend stalls.
 
 Scheduler (p1.pdf p.15, "balances loads across all requests"): an idle miner always
 gets the next job of the outstanding request that currently has the FEWEST jobs in
-flight (ties: oldest request first), so the workers assigned to each request differ by
-at most one whenever requests have work queued.
+flight (then the least work left, then the oldest), so the workers assigned to each
+request differ by at most one whenever requests have work queued.
 
-Failures (p1.pdf p.15): a lost miner's job goes back to the FRONT of its request's queue
-(and waits for a miner if none is left); a lost client's requests are dropped -- queued
-jobs are discarded, in-flight results are ignored when they arrive.  A job whose miners
-keep dying (more than MAX_REQUEUES losses, e.g. a job that trips a device fault on every
-GPU) is not handed to miner after miner: its request is abandoned and the client's
-connection closed, so the client prints "Disconnected".
+Failures (p1.pdf p.15): a lost miner's unfinished jobs go back to the FRONT of their
+requests' queues (unless another miner holds a copy); a lost client's requests are
+dropped -- queued jobs are discarded, in-flight results are ignored when they arrive.  A
+job whose miners keep dying while computing it (more than MAX_REQUEUES such losses, e.g.
+a job that trips a device fault on every GPU) is not handed to miner after miner: its
+request is abandoned and the client's connection closed, so the client prints
+"Disconnected".  Jobs queued behind the one a lost miner was computing never ran and are
+not charged.
 
 Validation: a Request is accepted only if 0 <= Lower <= Upper <= 2^64-1 (the uint64
 fields are already range-checked by unmarshal, as Go's json.Unmarshal would) and its

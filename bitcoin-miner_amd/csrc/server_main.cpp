@@ -10,20 +10,25 @@
 // compiled programs; it interoperates with the Python programs message for message.
 //
 //   gpuhash_server port
-//     GPUHASH_JOB_SIZE     nonces per job (default 2^34, ~0.5 s on one MI355X)
-//     GPUHASH_MINER_DEPTH  jobs a miner may hold at once (default 1; server.py's Scheduler)
-//     GPUHASH_SERVER_LOG   log joins, requests and failure handling to stderr
+//     GPUHASH_JOB_SIZE     nonces per job (default: about one LSP epoch of one MI355X, a
+//                          power of two: 2^36 at 2 s epochs; server.py default_job_size)
+//     GPUHASH_MINER_DEPTH  jobs a miner may hold at once (default 3)
+//     GPUHASH_COPIES       live copies of an overdue job (default 3; GPUHASH_BACKUP=0: 1)
+//     GPUHASH_SERVER_LOG   log joins, requests, copies and failure handling to stderr
 //     LSP_EPOCH_LIMIT / LSP_EPOCH_MILLIS / LSP_WINDOW_SIZE, LSPNET_SERVER_{READ,WRITE}_DROP
 //
 // Scheduling: an idle miner (fewest jobs held, then longest since its last job) gets the
 // next job of the request with the fewest jobs in flight, then the least work left to hand
 // out (shortest remaining first: a short request arriving while a long one holds every
-// miner is not kept waiting, and equal requests finish in turn), then the oldest.  Failures: a
-// lost miner's jobs go back to the front of their requests' queues, at most
-// MAX_REQUEUES times per job, after which the request is abandoned and its client
-// disconnected; a lost client's requests are dropped and late results ignored.  A
-// Request is served only if 0 <= Lower <= Upper <= 2^64-1 and Data fits the engine;
-// otherwise the client's connection is closed.  stdout is never written.
+// miner is not kept waiting, and equal requests finish in turn), then the oldest.  With
+// nothing left to hand out, a miner holding nothing gets a copy of a job every holder of
+// which is overdue by its learned rate.  Failures: a lost miner's
+// unfinished jobs go back to the front of their requests' queues unless a copy is out;
+// only the job it was computing counts toward that job's cap of MAX_REQUEUES, after
+// which the request is abandoned and its client disconnected; a lost client's requests
+// are dropped and late results ignored.  A Request is served only if
+// 0 <= Lower <= Upper <= 2^64-1 and Data fits the engine; otherwise the client's
+// connection is closed.  stdout is never written.
 #include <algorithm>
 #include <chrono>
 #include <cmath>

@@ -34,6 +34,26 @@ SHAPES = {
 }
 
 
+class SplitTail(bserver.Scheduler):
+    """A measured alternative (not the product): once less than one job per idle miner is
+    left to hand out, cut the request's remainder over the idle miners, down to
+    job_size / split_frac (policy key "split_frac")."""
+
+    def __init__(self, *a, split_frac: int = 4, **kw):
+        super().__init__(*a, **kw)
+        self.split_frac = split_frac
+
+    def size_for(self, miner, r):
+        size = self.job_size
+        idle = sum(1 for q in self.miners.values() if not q)
+        pend = sum(x.uncut() for x in self.requests.values() if x.has_pending())
+        if idle > 1 and pend < idle * size:
+            active = sum(1 for x in self.requests.values() if x.has_pending())
+            share = -(-r.uncut() // max(1, idle // max(1, active)))
+            size = max(size // self.split_frac, min(size, share))
+        return size
+
+
 def run(shape: str, policy: dict, seeds: int, epoch_ms: int, drop: float) -> dict:
     gpus, mpg, nclients, bits, kill = SHAPES[shape]
     params = lsp.NewParams()
@@ -42,8 +62,8 @@ def run(shape: str, policy: dict, seeds: int, epoch_ms: int, drop: float) -> dic
     ms, eff, avail, spec, disc = [], [], [], [], []
     for seed in range(seeds):
         kw = dict(policy)
-        r = lsp_des.run_system(bserver.Scheduler(**kw), gpus, mpg, reqs, params=params, drop=drop,
-                               kill=kill, seed=seed)
+        cls = SplitTail if "split_frac" in kw else bserver.Scheduler
+        r = lsp_des.run_system(cls(**kw), gpus, mpg, reqs, params=params, drop=drop, kill=kill, seed=seed)
         disc.append(r["disconnected"])  # LSP's own losses: 5 epochs of 19%-lossy silence
         ms.append(r["makespan"])
         eff.append(r["efficiency"])
