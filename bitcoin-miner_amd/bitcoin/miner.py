@@ -45,6 +45,7 @@ def run(hostport: str, engine=None, params=None, on_client=None) -> int:
     # GPUHASH_MINER_JOBLOG=1: one stderr line per job (wall-clock receive/start/end and the
     # engine's kernel ms), from which tools/system_bench.py measures how busy the GPU was
     joblog = os.environ.get("GPUHASH_MINER_JOBLOG", "") not in ("", "0")
+    _log(f"joined as connection {c.ConnID()} (pid {os.getpid()})")
     try:
         c.Write(marshal(NewJoin()))
         while True:

@@ -838,6 +838,12 @@ class Client {
         return conn_ != nullptr;
     }
 
+    // The connection ID the server assigned (0 before the connection is up).
+    long long conn_id() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return conn_ ? conn_->id() : 0;
+    }
+
     // Why the connection failed or was lost, with this loop's latest epoch ("" if it was not).
     std::string lost_reason() {
         std::lock_guard<std::mutex> lk(mu_);

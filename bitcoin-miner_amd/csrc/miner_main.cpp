@@ -29,6 +29,8 @@
 #include <string>
 #include <vector>
 
+#include <unistd.h>
+
 #include "gpuhash.h"
 #include "lsp_native.h"
 
@@ -92,6 +94,7 @@ int main(int argc, char** argv) {
     }
     int status = 0;
     long long jobs = 0;
+    logf("joined as connection %lld (pid %d)", client.conn_id(), (int)getpid());
     if (client.write(lspn::btc_marshal(BtcMsg{}))) {  // json.Marshal(bitcoin.NewJoin())
         std::string payload;
         while (client.read(payload)) {

@@ -267,7 +267,11 @@ def run_config5_full_size(procs, engine, oracle, golden, envf, kill_after, diag_
             "max_late_ms": {k: v["max_late_ms"] for k, v in late.items()},
             "late_epochs": {k: v["late_epochs"] for k, v in late.items() if v["late_epochs"]},
             "server_losses": [ln for ln in log.splitlines() if " lost" in ln or "abandoned" in ln],
-            "copies": sum(1 for ln in log.splitlines() if "copy of job" in ln)}
+            "copies": sum(1 for ln in log.splitlines() if "copy of job" in ln),
+            # each miner's exit status and its own account (its connection ID, why it ended)
+            "miners": [{"index": k, "returncode": m.returncode,
+                        "stderr": [ln for ln in e.splitlines() if "joined as" in ln or " lost" in ln
+                                   or "exiting" in ln or "rror" in ln][-6:]} for k, (m, e) in enumerate(zip(miners, merr))]}
     sysdiag.write_diag(diag_name, diag)
     print("config 5 diagnostics:", diag)
     return outs, [e for _, e in res], log, diag
