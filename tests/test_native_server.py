@@ -295,8 +295,18 @@ def test_jobs_must_fit_one_datagram_python_and_compiled(procs, plain_server, min
     assert "would not fit a 2000-byte LSP datagram" in log, log
 
 
+def test_overdue_copy_under_sanitizers(procs, server_bin, miner_bin, oracle):
+    """The compiled server's copy path (Job shared between miners' queues, the timed
+    read_until wake-up) under the plain, TSan and ASan + UBSan builds."""
+    _overdue_case(procs, server_bin, miner_bin, oracle, "compiled")
+
+
 @pytest.mark.parametrize("which", ["python", "compiled"])
 def test_overdue_job_is_copied_to_an_idle_miner(procs, plain_server, miner_bin, oracle, which):
+    _overdue_case(procs, plain_server, miner_bin, oracle, which)
+
+
+def _overdue_case(procs, plain_server, miner_bin, oracle, which):
     """Speculative copies (bitcoin/server.py Scheduler, csrc/server_main.cpp Scheduler): a
     miner that answered once and then sits on its next job forever -- its LSP connection
     alive, so the server never sees it lost -- does not hold that request up.  Once the
