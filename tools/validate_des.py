@@ -74,12 +74,19 @@ def main() -> None:
     args = ap.parse_args()
     for name in args.policies.split(","):
         extra, kw = POLICIES[name]
-        with cf.ThreadPoolExecutor(args.parallel) as ex:
-            runs = list(ex.map(lambda k: real_run(args, extra, k), range(args.runs)))
-        if args.out:
-            with open(args.out, "a") as f:
-                for r in runs:
+        def one(k):
+            r = real_run(args, extra, k)
+            # progress on stdout and the run's line in --out as each run ends (a GPU box
+            # kills a command that writes nothing for 3 minutes)
+            print(f"{name} run {k}: wall {r['wall_s']} s, busy {r['busy_frac_wall']}, "
+                  f"busy while available {r['busy_frac_avail']}", flush=True)
+            if args.out:
+                with open(args.out, "a") as f:
                     f.write(json.dumps(dict(r, policy=name)) + "\n")
+            return r
+
+        with cf.ThreadPoolExecutor(args.parallel) as ex:
+            runs = list(ex.map(one, range(args.runs)))
         # system_bench.py starts the clients 1.5 s (emulated) or 5 s (GPU) after the miners
         sims = model(kw, args.seeds, args.clients, args.bits, 1.5 if args.emulate else 5.0)
         work = args.clients * ((1 << args.bits) + 1)
