@@ -36,6 +36,7 @@ for step in "$@"; do
         go) { command -v go && go version; } > "$OUT/go.log" 2>&1; echo "go: $(cat $OUT/go.log)" ;;
         test) run pytest_gpu 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
         valid) run validate_des 900 python -u tools/validate_des.py --runs "${VALID_RUNS:-10}" --out "$OUT/r06_validate_des_runs.jsonl" ;;
+        validnew) run validate_des_defaults 900 python -u tools/validate_des.py --runs "${VALID_RUNS:-10}" --policies defaults --out "$OUT/r06_validate_des_runs_defaults2.jsonl" ;;
         valid37) run validate_des_2p37 600 python -u tools/validate_des.py --runs "${VALID_RUNS:-4}" --bits 37 --seeds 100 --out "$OUT/r06_validate_des_runs_2p37.jsonl" ;;
         c5ref) run c5ref 500 env GPUHASH_DIAG_DIR="$OUT/c5ref" python -u -m pytest tests/test_gpu_system.py -m gpu -x -v -s --timeout 450 --timeout-method thread -k reference_lsp_params ;;
         systest) run pytest_sys 600 python -u -m pytest tests/test_gpu_system.py -m gpu -x -v --timeout 300 --timeout-method thread ;;

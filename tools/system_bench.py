@@ -228,6 +228,10 @@ def main() -> None:
             "copies": len(jobs) - len(first),
             "client_done_s": sorted(round(t - t0_wall, 3) for t in done_at),
             "jobs_requeued": requeued, "all_results_verified": ok, "outputs": outs[:4],
+            # a client without a Result says why on stderr (its LSP's account)
+            "client_errors": {i: [ln for _, name, ln in lines[c.pid] if name == "err"][-4:]
+                              for i, (c, o) in enumerate(zip(clients, outs)) if not o.startswith("Result")},
+            "server_log_tail": log.splitlines()[-12:] if any(not o.startswith("Result") for o in outs) else [],
         }), flush=True)
     finally:
         for p in procs:
