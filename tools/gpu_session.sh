@@ -38,6 +38,7 @@ for step in "$@"; do
         valid) run validate_des 900 python -u tools/validate_des.py --runs "${VALID_RUNS:-10}" --out "$OUT/r06_validate_des_runs.jsonl" ;;
         validnew) run validate_des_defaults 900 python -u tools/validate_des.py --runs "${VALID_RUNS:-10}" --policies defaults --out "$OUT/r06_validate_des_runs_defaults2.jsonl" ;;
         valid37) run validate_des_2p37 600 python -u tools/validate_des.py --runs "${VALID_RUNS:-4}" --bits 37 --seeds 100 --out "$OUT/r06_validate_des_runs_2p37.jsonl" ;;
+        killprobe) run kill_probe 400 python -u tools/kill_probe.py --rounds "${KILL_ROUNDS:-4}" ;;
         c5ref) run c5ref 500 env GPUHASH_DIAG_DIR="$OUT/c5ref" python -u -m pytest tests/test_gpu_system.py -m gpu -x -v -s --timeout 450 --timeout-method thread -k reference_lsp_params ;;
         systest) run pytest_sys 600 python -u -m pytest tests/test_gpu_system.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
