@@ -39,7 +39,8 @@ def stats(xs: list[float]) -> dict:
 
 def real_run(args, extra: list[str], k: int) -> dict:
     cmd = [sys.executable, os.path.join(ROOT, "tools", "system_bench.py"), "--clients", str(args.clients),
-           "--bits", str(args.bits), "--miners", "1", "--kill-after", "-1", "--label", f"run {k}"] + extra
+           "--bits", str(args.bits), "--miners", str(args.miners), "--kill-after", str(args.kill_after),
+           "--label", f"run {k}"] + extra
     if args.emulate:
         cmd += ["--emulate", str(GPU)]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
@@ -48,16 +49,18 @@ def real_run(args, extra: list[str], k: int) -> dict:
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
-def model(policy, seeds: int, clients: int, bits: int, client_start: float) -> list[dict]:
+def model(policy, seeds: int, clients: int, bits: int, client_start: float, miners: int = 1,
+          kill_after: float = -1.0) -> list[dict]:
     import lsp
     import lsp_des
     from bitcoin import server as bserver
     reqs = [(f"client-{i:02d}", 0, 1 << bits) for i in range(clients)]
+    kill = (kill_after, miners - 1) if kill_after >= 0 and miners > 1 else None  # system_bench kills the last
     out = []
     for s in range(seeds):
         sch = bserver.make_scheduler(epoch_s=2.0) if policy is None else bserver.Scheduler(**policy)
-        out.append(lsp_des.run_system(sch, [GPU], 1, reqs, params=lsp.NewParams(), drop=0.10, seed=s,
-                                      client_start=client_start))
+        out.append(lsp_des.run_system(sch, [GPU] * miners, 1, reqs, params=lsp.NewParams(), drop=0.10, seed=s,
+                                      client_start=client_start, kill=kill))
     return out
 
 
@@ -69,6 +72,8 @@ def main() -> None:
     ap.add_argument("--emulate", action="store_true")
     ap.add_argument("--clients", type=int, default=4)
     ap.add_argument("--bits", type=int, default=35)
+    ap.add_argument("--miners", type=int, default=1, help="one GPU each (emulated: one 34.6 GH/s miner each)")
+    ap.add_argument("--kill-after", type=float, default=-1.0, help="SIGKILL the last miner this long after the clients start")
     ap.add_argument("--policies", default="round5,defaults")
     ap.add_argument("--out", default=None, help="also append each real run's line here")
     args = ap.parse_args()
@@ -88,15 +93,19 @@ def main() -> None:
         with cf.ThreadPoolExecutor(args.parallel) as ex:
             runs = list(ex.map(one, range(args.runs)))
         # system_bench.py starts the clients 1.5 s (emulated) or 5 s (GPU) after the miners
-        sims = model(kw, args.seeds, args.clients, args.bits, 1.5 if args.emulate else 5.0)
+        sims = model(kw, args.seeds, args.clients, args.bits, 1.5 if args.emulate else 5.0, args.miners,
+                     args.kill_after)
         work = args.clients * ((1 << args.bits) + 1)
         print(json.dumps({
             "policy": name, "miners": "emulated (sleep n/34.6e9)" if args.emulate else "GPU",
-            "shape": f"1 miner, {args.clients} clients x [0, 2^{args.bits}], 2 s epochs, limit 5, 10% drops",
+            "shape": f"{args.miners} miner(s), {args.clients} clients x [0, 2^{args.bits}], 2 s epochs, limit 5, "
+                     f"10% drops" + (f", last miner killed {args.kill_after} s in" if args.kill_after >= 0 else ""),
             "real_makespan_s": stats([r["wall_s"] for r in runs]),
             "model_makespan_s": stats([s["makespan"] for s in sims]),
+            "real_GHs": stats([work / r["wall_s"] / 1e9 for r in runs]),
+            "model_GHs": stats([work / s["makespan"] / 1e9 for s in sims]),
             "real_busy_frac_wall": stats([r["busy_frac_wall"] for r in runs]),
-            "model_busy_frac_wall": stats([work / GPU / s["makespan"] for s in sims]),
+            "model_busy_frac_wall": stats([work / GPU / args.miners / s["makespan"] for s in sims]),
             "real_busy_frac_avail": stats([r["busy_frac_avail"] or 0.0 for r in runs]),
             "model_busy_frac_avail": stats([s["busy_avail"] for s in sims]),
             "real_all_verified": all(r["all_results_verified"] in (True, None) for r in runs),
