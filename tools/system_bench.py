@@ -61,6 +61,8 @@ def main() -> None:
     ap.add_argument("--no-backup", action="store_true", help="GPUHASH_BACKUP=0: no speculative copies")
     ap.add_argument("--copies", type=int, default=None, help="GPUHASH_COPIES (default: the server's)")
     ap.add_argument("--label", default="", help="free text copied to the output line")
+    ap.add_argument("--compiled-server", action="store_true",
+                    help="the server is lib/gpuhash_server (miners and clients as chosen otherwise)")
     ap.add_argument("--emulate", type=float, default=0.0,
                     help="miners are tools/emu_miner.py sleeping n/RATE per job (CPU-only; no verification)")
     ap.add_argument("--gpus", type=int, default=None,
@@ -105,8 +107,8 @@ def main() -> None:
             senv["GPUHASH_JOB_SECONDS"] = "0.5"
         elif args.job_bits:
             senv["GPUHASH_JOB_SIZE"] = str(1 << args.job_bits)
-        if args.compiled:
-            args.native = True
+        if args.compiled or args.compiled_server:
+            args.native = args.native or args.compiled
             server = start([os.path.join(LIB, "gpuhash_server"), str(port)], native=True, env=senv)
         else:
             server = start([os.path.join(BIN, "server"), str(port)], env=senv)

@@ -43,6 +43,8 @@ def real_run(args, extra: list[str], k: int) -> dict:
            "--label", f"run {k}"] + extra
     if args.emulate:
         cmd += ["--emulate", str(GPU)]
+    if args.compiled_server:
+        cmd += ["--compiled-server"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     if out.returncode != 0:
         raise RuntimeError(out.stderr[-2000:])
@@ -76,6 +78,7 @@ def main() -> None:
     ap.add_argument("--kill-after", type=float, default=-1.0, help="SIGKILL the last miner this long after the clients start")
     ap.add_argument("--policies", default="round5,defaults")
     ap.add_argument("--out", default=None, help="also append each real run's line here")
+    ap.add_argument("--compiled-server", action="store_true", help="lib/gpuhash_server instead of bin/server")
     args = ap.parse_args()
     for name in args.policies.split(","):
         extra, kw = POLICIES[name]
@@ -98,6 +101,7 @@ def main() -> None:
         work = args.clients * ((1 << args.bits) + 1)
         print(json.dumps({
             "policy": name, "miners": "emulated (sleep n/34.6e9)" if args.emulate else "GPU",
+            "server": "lib/gpuhash_server" if args.compiled_server else "bin/server",
             "shape": f"{args.miners} miner(s), {args.clients} clients x [0, 2^{args.bits}], 2 s epochs, limit 5, "
                      f"10% drops" + (f", last miner killed {args.kill_after} s in" if args.kill_after >= 0 else ""),
             "real_makespan_s": stats([r["wall_s"] for r in runs]),
