@@ -3,12 +3,15 @@ pp.13-15: split each client Request into jobs, farm them to miners, merge the Re
 answer the client.
 
 Job chunking: the reference leaves "a suitable maximum job size"
-open.  Default: fixed jobs of about one LSP epoch of one MI355X, a power of two --
-2^36 nonces at the reference's 2 s epochs (default_job_size).  Each job is a Request and
-a Result over a window-1 connection whose dropped messages wait for the next epoch, so
-jobs much shorter than an epoch leave the GPU waiting on the connection; a request's
-last sliver (under a quarter job) rides with the job before it.  GPUHASH_JOB_SIZE
-overrides the size.
+open.  Default: fixed jobs of half a second of one MI355X (or one LSP epoch if shorter),
+a power of two -- 2^34 nonces at the reference's 2 s epochs (default_job_size).  The
+programs send every LSP datagram three times (bitcoin.SEND_COPIES), so a dropped Request
+or Result rarely waits for the next epoch, and four jobs per 2^36-nonce config-5 request
+spread it over a node's GPUs.  With single sends (LSP_SEND_COPIES=1, the protocol exactly
+as specified) a dropped message stalls its window-1 connection until the next epoch
+with p = 0.19 at config 5's drops, and jobs are one epoch long (2^36) so that the
+stalls do not dominate.  A request's last sliver (under a quarter job) rides with the
+job before it.  GPUHASH_JOB_SIZE overrides the size.
 
 Depth and speculative copies: a miner holds up to MINER_DEPTH (3) jobs, so its next
 Request is already there while a Result or a Request waits for a resend; when nothing is
@@ -78,16 +81,20 @@ SLACK = 0.1        # a copy is overdue this long after its expected answer ...
 SLACK_FRAC = 0.25  # ... or this fraction of its job time, if longer
 
 
-def default_job_size(epoch_s: float) -> int:
-    """About one LSP epoch of one MI355X, to a power of two: 2^36 at the reference's 2 s
-    epochs, 2^33 at 200 ms.  Each job is a Request and a Result over a window-1 connection
-    whose dropped messages wait for the next epoch, so a job much shorter than an epoch
-    spends its time waiting on the connection."""
-    b = math.floor(math.log2(max(1.0, REF_RATE * epoch_s)) + 0.5)  # lround, as the C++ server
+def default_job_size(epoch_s: float, send_copies: int = 1) -> int:
+    """GPU work of one MI355X, to a power of two, for a job's wall time of: one LSP epoch
+    when every datagram is sent once (2^36 at the reference's 2 s epochs, 2^33 at 200 ms)
+    -- each job is a Request and a Result over a window-1 connection whose dropped
+    messages wait for the next epoch, so a job much shorter than an epoch spends its time
+    waiting on the connection; half a second, or one epoch if shorter, when the programs
+    send copies (2^34 at 2 s, 2^33 at 200 ms) -- a stall is then rare, and shorter jobs
+    spread config 5's 2^36-nonce requests over a node's GPUs."""
+    secs = epoch_s if send_copies <= 1 else min(epoch_s, 0.5)
+    b = math.floor(math.log2(max(1.0, REF_RATE * secs)) + 0.5)  # lround, as the C++ server
     return 1 << min(40, max(30, b))
 
 
-DEFAULT_JOB_SIZE = default_job_size(2.0)  # 2^36 at lsp.params' DefaultEpochMillis
+DEFAULT_JOB_SIZE = default_job_size(2.0)  # 2^36 at lsp.params' DefaultEpochMillis, one copy
 
 
 @dataclass
@@ -537,9 +544,9 @@ class ServerCore:
         self.dispatch()
 
 
-def make_scheduler(job_size: int | None = None, epoch_s: float = 2.0) -> Scheduler:
+def make_scheduler(job_size: int | None = None, epoch_s: float = 2.0, send_copies: int = 1) -> Scheduler:
     """The Scheduler serve() runs (csrc/server_main.cpp builds the same one): jobs of
-    default_job_size(epoch_s), MINER_DEPTH jobs per miner, up to COPIES live copies of an
+    default_job_size(epoch_s, send_copies), MINER_DEPTH jobs per miner, up to COPIES live copies of an
     overdue job.  GPUHASH_JOB_SIZE, GPUHASH_JOB_SECONDS (per-miner sizing),
     GPUHASH_MINER_DEPTH, GPUHASH_COPIES and GPUHASH_BACKUP=0 override them."""
     secs = os.environ.get("GPUHASH_JOB_SECONDS")
@@ -548,7 +555,7 @@ def make_scheduler(job_size: int | None = None, epoch_s: float = 2.0) -> Schedul
     kw = dict(depth=depth, copies=copies, hedge="overdue", slack=SLACK, slack_frac=SLACK_FRAC)
     if job_size is None and secs:
         return Scheduler(sizing=Sizing(target_s=float(secs)), **kw)
-    size = job_size or int(os.environ.get("GPUHASH_JOB_SIZE", 0)) or default_job_size(epoch_s)
+    size = job_size or int(os.environ.get("GPUHASH_JOB_SIZE", 0)) or default_job_size(epoch_s, send_copies)
     return Scheduler(size, **kw)
 
 
@@ -562,7 +569,8 @@ def serve(port: int, params=None, job_size: int | None = None, ready=None, log=N
             print(f"server: {line}", file=sys.stderr, flush=True)
     if ready is not None:
         ready(srv)
-    core = ServerCore(make_scheduler(job_size, params.EpochMillis / 1000.0), srv.Write, srv.CloseConn, log)
+    sched = make_scheduler(job_size, params.EpochMillis / 1000.0, params.SendCopies)
+    core = ServerCore(sched, srv.Write, srv.CloseConn, log)
     while True:
         wake = core.sched.next_wakeup()
         try:

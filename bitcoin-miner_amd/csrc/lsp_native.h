@@ -572,6 +572,9 @@ struct Params {  // lsp/params.go:8-35, with the env overrides of bitcoin.params
     int epoch_limit = env_int("LSP_EPOCH_LIMIT", 5);
     int epoch_ms = env_int("LSP_EPOCH_MILLIS", 2000);
     int window = env_int("LSP_WINDOW_SIZE", 1);
+    // not in params.go: times each originated datagram is sent (bitcoin.SEND_COPIES; 1 is
+    // the protocol exactly as specified; lsp/endpoint.py has the rule)
+    int send_copies = std::max(1, env_int("LSP_SEND_COPIES", 3));
 };
 
 using Addr = std::pair<uint32_t, uint16_t>;  // IPv4 address and port, network order
@@ -659,7 +662,8 @@ class Udp {
 class Conn {
    public:
     Conn(long long id, const Params& p, std::function<void(const LspMsg&)> send)
-        : id_(id), w_(std::max(1, p.window)), k_(std::max(1, p.epoch_limit)), send_(std::move(send)) {}
+        : id_(id), w_(std::max(1, p.window)), k_(std::max(1, p.epoch_limit)), copies_(std::max(1, p.send_copies)),
+          send_(std::move(send)) {}
 
     long long id() const { return id_; }
     bool lost() const { return lost_; }
@@ -682,8 +686,12 @@ class Conn {
             return;
         }
         if (m.type != MsgData) return;
-        send_(LspMsg{MsgAck, id_, m.seq, false, {}});
-        if (m.seq >= expected_ && m.seq < expected_ + w_ && !rbuf_.count(m.seq)) {
+        const bool fresh = m.seq >= expected_ && m.seq < expected_ + w_ && !rbuf_.count(m.seq);
+        if (fresh)
+            send_copies(LspMsg{MsgAck, id_, m.seq, false, {}});
+        else
+            send_(LspMsg{MsgAck, id_, m.seq, false, {}});  // a duplicate: acked again, once
+        if (fresh) {
             rbuf_.emplace(m.seq, m.payload);
             recent_.push_back(m.seq);
             if ((int)recent_.size() > w_) recent_.pop_front();
@@ -715,9 +723,9 @@ class Conn {
                            " ms ago";
             return true;
         }
-        if (!got_data_) send_(LspMsg{MsgAck, id_, 0, false, {}});
-        for (auto& [seq, payload] : unacked_) send_(LspMsg{MsgData, id_, seq, true, payload});
-        for (long long seq : recent_) send_(LspMsg{MsgAck, id_, seq, false, {}});
+        if (!got_data_) send_copies(LspMsg{MsgAck, id_, 0, false, {}});
+        for (auto& [seq, payload] : unacked_) send_copies(LspMsg{MsgData, id_, seq, true, payload});
+        for (long long seq : recent_) send_copies(LspMsg{MsgAck, id_, seq, false, {}});
         return false;
     }
     void heard() {
@@ -727,7 +735,7 @@ class Conn {
 
    private:
     long long id_;
-    int w_, k_;
+    int w_, k_, copies_;
     std::function<void(const LspMsg&)> send_;
     bool lost_ = false, got_data_ = false;
     bool heard_ = true;  // heard from the peer since the last epoch
@@ -750,9 +758,14 @@ class Conn {
         while (!pending_.empty() && pending_.front().first < base + w_) {
             auto [seq, payload] = std::move(pending_.front());
             pending_.pop_front();
-            send_(LspMsg{MsgData, id_, seq, true, payload});
+            send_copies(LspMsg{MsgData, id_, seq, true, payload});
             unacked_.emplace(seq, std::move(payload));
         }
+    }
+    // a message this side originates, and the ack of a Data message seen for the first
+    // time, go out copies_ times; a duplicate is acked once (lsp/endpoint.py)
+    void send_copies(const LspMsg& m) {
+        for (int i = 0; i < copies_; i++) send_(m);
     }
 };
 
@@ -829,7 +842,7 @@ class Client {
     // Blocks until the server acknowledges the connection (or EpochLimit epochs pass).
     bool connect(const std::string& hostport) {
         if (!udp_.dial(hostport)) return false;
-        udp_.write(lsp_marshal(LspMsg{MsgConnect, 0, 0, false, {}}), udp_.peer());
+        send_connect();
         thread_ = std::thread([this] {
             event_loop(udp_.fd(), p_.epoch_ms, mu_, stop_, late_, "lsp-client", [this](bool e) { tick(e); });
         });
@@ -899,6 +912,11 @@ class Client {
         if (thread_.joinable()) thread_.join();
     }
 
+    void send_connect() {
+        for (int i = 0; i < std::max(1, p_.send_copies); i++)
+            udp_.write(lsp_marshal(LspMsg{MsgConnect, 0, 0, false, {}}), udp_.peer());
+    }
+
     void tick(bool is_epoch) {  // mu_ held
         std::string raw;
         Addr from;
@@ -925,7 +943,7 @@ class Client {
                 failed_ = true;
                 cv_.notify_all();
             } else {
-                udp_.write(lsp_marshal(LspMsg{MsgConnect, 0, 0, false, {}}), udp_.peer());
+                send_connect();
             }
             return;
         }

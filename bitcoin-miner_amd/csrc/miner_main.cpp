@@ -13,7 +13,8 @@
 // It interoperates with the Python server and client (bitcoin-miner_amd/bitcoin/).
 //
 //   gpuhash_miner host:port         (GPUHASH_DEVICES=0,1 narrows the devices;
-//                                    LSP_EPOCH_LIMIT / LSP_EPOCH_MILLIS / LSP_WINDOW_SIZE)
+//                                    LSP_EPOCH_LIMIT / LSP_EPOCH_MILLIS / LSP_WINDOW_SIZE /
+//                                    LSP_SEND_COPIES)
 //
 // Failure rules (as bitcoin/miner.py): an empty range (Lower > Upper) is answered with
 // (2^64-1, 2^64-1), the identity of the server's (hash, nonce) merge; every engine error

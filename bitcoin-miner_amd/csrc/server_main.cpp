@@ -10,12 +10,14 @@
 // compiled programs; it interoperates with the Python programs message for message.
 //
 //   gpuhash_server port
-//     GPUHASH_JOB_SIZE     nonces per job (default: about one LSP epoch of one MI355X, a
-//                          power of two: 2^36 at 2 s epochs; server.py default_job_size)
+//     GPUHASH_JOB_SIZE     nonces per job (default: half a second of one MI355X, or one
+//                          LSP epoch if shorter, a power of two: 2^34 at 2 s epochs; one
+//                          epoch, 2^36, with LSP_SEND_COPIES=1; server.py default_job_size)
 //     GPUHASH_MINER_DEPTH  jobs a miner may hold at once (default 3)
 //     GPUHASH_COPIES       live copies of an overdue job (default 3; GPUHASH_BACKUP=0: 1)
 //     GPUHASH_SERVER_LOG   log joins, requests, copies and failure handling to stderr
-//     LSP_EPOCH_LIMIT / LSP_EPOCH_MILLIS / LSP_WINDOW_SIZE, LSPNET_SERVER_{READ,WRITE}_DROP
+//     LSP_EPOCH_LIMIT / LSP_EPOCH_MILLIS / LSP_WINDOW_SIZE, LSP_SEND_COPIES (default 3),
+//     LSPNET_SERVER_{READ,WRITE}_DROP
 //
 // Scheduling: an idle miner (fewest jobs held, then longest since its last job) gets the
 // next job of the request with the fewest jobs in flight, then the least work left to hand
@@ -58,9 +60,11 @@ constexpr int kDefaultCopies = 3;
 constexpr double kSlack = 0.1;
 constexpr double kSlackFrac = 0.25;
 
-// about one LSP epoch of one MI355X, to a power of two (server.py default_job_size)
-uint64_t default_job_size(double epoch_s) {
-    long b = std::lround(std::log2(std::max(1.0, kRefRate * epoch_s)));
+// GPU work of one MI355X for one LSP epoch (datagrams sent once), or for half a second or
+// one epoch if shorter (sent in copies), to a power of two (server.py default_job_size)
+uint64_t default_job_size(double epoch_s, int send_copies) {
+    const double secs = send_copies <= 1 ? epoch_s : std::min(epoch_s, 0.5);
+    long b = std::lround(std::log2(std::max(1.0, kRefRate * secs)));
     return 1ull << std::min(40L, std::max(30L, b));
 }
 
@@ -449,7 +453,7 @@ int main(int argc, char** argv) {
     }
     const char* backup = std::getenv("GPUHASH_BACKUP");
     const int copies = backup && std::strcmp(backup, "0") == 0 ? 1 : (int)env_u64("GPUHASH_COPIES", kDefaultCopies);
-    Scheduler sched(env_u64("GPUHASH_JOB_SIZE", default_job_size(params.epoch_ms / 1000.0)),
+    Scheduler sched(env_u64("GPUHASH_JOB_SIZE", default_job_size(params.epoch_ms / 1000.0, params.send_copies)),
                     (int)env_u64("GPUHASH_MINER_DEPTH", kDefaultDepth),
                     copies, kSlack, kSlackFrac);
 

@@ -34,7 +34,7 @@ class Client:
         self._loop = Loop(self._conn, self._p.EpochMillis, self._on_datagram, self._on_command,
                           self._on_epoch, role="lsp-client")
         self._loop.start()
-        self._send(NewConnect())
+        self._send_connect()
         self._connected.wait()
         if self._failed:
             self._shutdown()
@@ -73,6 +73,10 @@ class Client:
     def _send(self, m: Message) -> None:
         self._conn.write_to(m.marshal())
 
+    def _send_connect(self) -> None:
+        for _ in range(max(1, self._p.SendCopies)):
+            self._send(NewConnect())
+
     def _on_datagram(self, data: bytes, addr) -> None:
         # only the server's datagrams: the reference's lspnet.DialUDP is a connected UDP
         # socket, which the kernel filters by source (csrc/lsp_native.h does the same)
@@ -85,7 +89,8 @@ class Client:
         if self._st is None:
             if m.Type == MsgType.MsgAck and m.SeqNum == 0 and m.ConnID > 0:
                 self._conn_id = m.ConnID
-                self._st = ConnState(m.ConnID, self._p.WindowSize, self._p.EpochLimit, self._send)
+                self._st = ConnState(m.ConnID, self._p.WindowSize, self._p.EpochLimit, self._send,
+                                     self._p.SendCopies)
                 self._connected.set()
             return
         if m.ConnID != self._conn_id:
@@ -110,7 +115,7 @@ class Client:
                 self.lost_reason = f"no connect ack in {self._connect_silent} epochs"
                 self._connected.set()
             else:
-                self._send(NewConnect())
+                self._send_connect()
             return
         was_lost = self._st.lost
         self._st.on_epoch()

@@ -10,6 +10,16 @@ lsp/server_impl.go, which cannot carry data as written -- SURVEY.md 2 rows 8-9):
     if no data has been received yet (heartbeat / connect ack), and count the epoch as
     silent unless something arrived; K silent epochs => connection lost.
 
+Send copies (Params.SendCopies, an extension; 1 = the protocol exactly as p1.pdf
+specifies it): every message this side originates -- a Data message when it enters the
+window, the ack of a Data message seen for the first time, and each epoch's resends,
+re-acks and heartbeat -- goes out that many times back to back; a duplicate (a copy, or
+a resend) is acked once.  The receiver already treats the copies as the duplicates an
+epoch resend makes (ack again, deliver once), so the wire protocol is unchanged.  On a
+link that drops each datagram with probability p, a message then holds up its window
+until the next epoch with probability about 2 p^copies (its copies, or the acks of the
+first to arrive, all lost) instead of 1 - (1 - p)^2.
+
 Like the reference's design (one handleMessages goroutine per endpoint), one loop
 thread owns all protocol state; API calls post commands to it through a queue.
 
@@ -36,11 +46,12 @@ from .message import Message, MsgType, NewAck, NewData
 class ConnState:
     """One side of one connection."""
 
-    def __init__(self, conn_id: int, window: int, epoch_limit: int, send):
+    def __init__(self, conn_id: int, window: int, epoch_limit: int, send, copies: int = 1):
         self.conn_id = conn_id
         self.w = max(1, window)
         self.k = max(1, epoch_limit)
         self.send = send                     # send(Message)
+        self.copies = max(1, copies)         # times each originated message is sent
         self.next_seq = 1                    # next data seq to assign
         self.pending = collections.deque()   # (seq, payload) not yet inside the window
         self.unacked = {}                    # seq -> payload, sent and not acked
@@ -68,7 +79,11 @@ class ConnState:
         while self.pending and self.pending[0][0] < base + self.w:
             seq, payload = self.pending.popleft()
             self.unacked[seq] = payload
-            self.send(NewData(self.conn_id, seq, payload))
+            self._send_copies(NewData(self.conn_id, seq, payload))
+
+    def _send_copies(self, m: Message) -> None:
+        for _ in range(self.copies):
+            self.send(m)
 
     def write(self, payload: bytes) -> None:
         self.pending.append((self.next_seq, payload))
@@ -89,9 +104,13 @@ class ConnState:
             return []
         if m.Type != MsgType.MsgData:
             return []
-        self.send(NewAck(self.conn_id, m.SeqNum))
+        new = m.SeqNum >= self.expected and m.SeqNum not in self.rbuf and m.SeqNum < self.expected + self.w
+        if new:
+            self._send_copies(NewAck(self.conn_id, m.SeqNum))
+        else:
+            self.send(NewAck(self.conn_id, m.SeqNum))  # a duplicate: acked again, once
         out = []
-        if m.SeqNum >= self.expected and m.SeqNum not in self.rbuf and m.SeqNum < self.expected + self.w:
+        if new:
             self.rbuf[m.SeqNum] = m.Payload or b""
             self.recent.append(m.SeqNum)
             self.got_data = True
@@ -126,11 +145,11 @@ class ConnState:
                                 f"{1000 * (time.monotonic() - self.last_heard):.0f} ms ago")
             return
         if not self.got_data:
-            self.send(NewAck(self.conn_id, 0))
+            self._send_copies(NewAck(self.conn_id, 0))
         for seq in sorted(self.unacked):
-            self.send(NewData(self.conn_id, seq, self.unacked[seq]))
+            self._send_copies(NewData(self.conn_id, seq, self.unacked[seq]))
         for seq in self.recent:
-            self.send(NewAck(self.conn_id, seq))
+            self._send_copies(NewAck(self.conn_id, seq))
 
 
 class Loop:

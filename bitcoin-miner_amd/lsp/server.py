@@ -106,7 +106,8 @@ class Server:
                 self._next_id += 1
                 self._id_of[addr] = cid
                 self._addr_of[cid] = addr
-                self._conns[cid] = ConnState(cid, self._p.WindowSize, self._p.EpochLimit, self._sender(addr))
+                self._conns[cid] = ConnState(cid, self._p.WindowSize, self._p.EpochLimit, self._sender(addr),
+                                             self._p.SendCopies)
             st = self._conns.get(cid)
             if st is not None:
                 st.mark_heard()

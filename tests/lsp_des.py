@@ -108,7 +108,7 @@ class ServerEP(Endpoint):
                 self.id_of[id(src)] = cid
                 self.peer[cid] = src
                 self.conns[cid] = ConnState(cid, self.p.WindowSize, self.p.EpochLimit,
-                                            lambda x, d=src: self.net.send(self, d, x))
+                                            lambda x, d=src: self.net.send(self, d, x), self.p.SendCopies)
             st = self.conns.get(cid)
             if st is not None:
                 st.mark_heard()
@@ -158,7 +158,11 @@ class ClientEP(Endpoint):
         self.st: ConnState | None = None
         self.connect_silent = 0
         self.closing = False
-        self.net.send(self, server, NewConnect())
+        self._connect()
+
+    def _connect(self) -> None:
+        for _ in range(max(1, self.p.SendCopies)):
+            self.net.send(self, self.server, NewConnect())
 
     def on_datagram(self, src, m) -> None:
         if src is not self.server:
@@ -166,7 +170,7 @@ class ClientEP(Endpoint):
         if self.st is None:
             if m.Type == MsgType.MsgAck and m.SeqNum == 0 and m.ConnID > 0:
                 self.st = ConnState(m.ConnID, self.p.WindowSize, self.p.EpochLimit,
-                                    lambda x: self.net.send(self, self.server, x))
+                                    lambda x: self.net.send(self, self.server, x), self.p.SendCopies)
                 self.app.on_connected()
             return
         if m.ConnID != self.st.conn_id:
@@ -182,7 +186,7 @@ class ClientEP(Endpoint):
                 self.dead = True
                 self.app.on_lost()
             else:
-                self.net.send(self, self.server, NewConnect())
+                self._connect()
             return
         was = self.st.lost
         self.st.on_epoch()

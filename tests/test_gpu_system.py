@@ -329,24 +329,29 @@ def env_reference(**extra):
 
 
 @pytest.mark.timeout(900)
-def test_config5_full_size_reference_lsp_params(procs, engine, oracle, golden):
+@pytest.mark.parametrize("send_copies", [None, 1], ids=["send_copies_default", "single_sends"])
+def test_config5_full_size_reference_lsp_params(procs, engine, oracle, golden, send_copies):
     """config 5 at full size at the untouched protocol's parameters
     (lsp/params.go:9-11: 2000 ms epochs, EpochLimit 5, window 1), 10% drops on every role,
     a miner SIGKILLed 4 s in (LSP notices it 10 s later; the server copies its overdue
     jobs before then).  Every Result must equal its golden.
 
-    At these parameters LSP itself gives up on a connection now and then: a client whose
-    Connect or its Ack is lost five times running (each gets through with 0.9^2, so
-    (1 - 0.81^2)^5 = 0.5% per client, 7.5% that one of 16 does) or that hears nothing for
-    5 whole epochs prints "Disconnected", as the reference's client would
-    (tests/test_scheduler_sim.py measures both rates through the protocol model).  One such
-    client is accepted only with LSP's own reason on its stderr; the server must abandon
-    nothing."""
-    outs, errs, log, diag = run_config5_full_size(procs, engine, oracle, golden, env_reference, 4.0,
-                                                  "config5_reference_params_diag.json")
+    Twice: with the programs' default of sending each datagram three times
+    (bitcoin.SEND_COPIES), where every client must get its Result; and with every
+    datagram sent once (LSP_SEND_COPIES=1, the protocol exactly as specified), where LSP
+    itself gives up on a connection now and then: a client whose Connect or its Ack is
+    lost five times running (each gets through with 0.9^2, so (1 - 0.81^2)^5 = 0.5% per
+    client, 7.5% that one of 16 does) or that hears nothing for 5 whole epochs prints
+    "Disconnected", as the reference's client would (tests/test_scheduler_sim.py measures
+    both rates through the protocol model).  One such client is accepted there only with
+    LSP's own reason on its stderr; the server must abandon nothing."""
+    extra = {} if send_copies is None else {"LSP_SEND_COPIES": send_copies}
+    name = "config5_reference_params_diag.json" if send_copies is None else "config5_reference_params_single_diag.json"
+    outs, errs, log, diag = run_config5_full_size(procs, engine, oracle, golden,
+                                                  lambda **kw: env_reference(**extra, **kw), 4.0, name)
     gave_up = [i for i in diag["failed_clients"] if outs[i] == "Disconnected" and LSP_GAVE_UP.search(errs[i])]
-    assert len(gave_up) <= 1 and set(gave_up) == set(diag["failed_clients"]), diag
+    assert len(gave_up) <= (1 if send_copies == 1 else 0) and set(gave_up) == set(diag["failed_clients"]), diag
     assert "abandoned" not in log, log[-3000:]
     assert check_config5(outs, golden, oracle, skip=set(gave_up)) == 16 - len(gave_up)
-    print(f"config 5 full size at the reference's LSP params: {diag['GHs']} GH/s, "
-          f"{diag['copies']} speculative copies")
+    print(f"config 5 full size at the reference's LSP params ({send_copies or 'default'} send copies): "
+          f"{diag['GHs']} GH/s, {diag['copies']} speculative copies")

@@ -48,9 +48,9 @@ def echo_server(params):
     return srv, stop, t
 
 
-def run_echo(nclients, nmsgs, params, drop=0):
+def run_echo(nclients, nmsgs, params, drop=0, client_params=None):
     srv, stop, t = echo_server(params)
-    clients = [lsp.NewClient(f"127.0.0.1:{srv.port}", params) for _ in range(nclients)]
+    clients = [lsp.NewClient(f"127.0.0.1:{srv.port}", client_params or params) for _ in range(nclients)]
     assert len({c.ConnID() for c in clients}) == nclients
     lspnet.SetWriteDropPercent(drop)
     errors = []
@@ -95,6 +95,48 @@ def test_window_sizes(window):
 @pytest.mark.parametrize("drop", [10, 20])
 def test_robust_with_write_drops(drop):
     run_echo(4, 25, lsp.Params(EpochLimit=20, EpochMillis=20, WindowSize=4), drop=drop)
+
+
+@pytest.mark.parametrize("copies,window", [(2, 1), (3, 1), (3, 4)])
+def test_send_copies_deliver_once_in_order(copies, window):
+    """SendCopies (lsp/endpoint.py): every originated datagram goes out `copies` times; the
+    receiver must still deliver each message exactly once, in order, under drops."""
+    p = lsp.Params(EpochLimit=20, EpochMillis=20, WindowSize=window, SendCopies=copies)
+    run_echo(4, 25, p, drop=20)
+
+
+@pytest.mark.parametrize("server_copies,client_copies", [(1, 3), (3, 1)])
+def test_send_copies_interoperate_with_single_sends(server_copies, client_copies):
+    """A peer that sends copies talks to one that sends each datagram once (the protocol
+    as specified, e.g. the reference's own endpoints): the copies are duplicates it
+    already handles."""
+    p = dict(EpochLimit=20, EpochMillis=20, WindowSize=1)
+    run_echo(3, 20, lsp.Params(SendCopies=server_copies, **p), drop=15,
+             client_params=lsp.Params(SendCopies=client_copies, **p))
+
+
+def test_send_copies_count():
+    """What goes out: a Data message `copies` times; its ack `copies` times the first time
+    it arrives and once per later duplicate; each epoch's resends, re-acks and heartbeats
+    `copies` times."""
+    from lsp.endpoint import ConnState
+    sent = []
+    a = ConnState(1, 1, 5, sent.append, copies=3)
+    a.write(b"x")
+    assert [(m.Type, m.SeqNum) for m in sent] == [(lsp.MsgType.MsgData, 1)] * 3
+    sent.clear()
+    b_sent = []
+    b = ConnState(1, 1, 5, b_sent.append, copies=3)
+    assert b.on_message(lsp.NewData(1, 1, b"x")) == [b"x"]
+    assert b.on_message(lsp.NewData(1, 1, b"x")) == []  # a copy: acked again, not delivered
+    assert [(m.Type, m.SeqNum) for m in b_sent] == [(lsp.MsgType.MsgAck, 1)] * 4
+    b_sent.clear()
+    b.on_epoch()  # re-ack the last received message, three times
+    assert [(m.Type, m.SeqNum) for m in b_sent] == [(lsp.MsgType.MsgAck, 1)] * 3
+    a.on_epoch()  # unacked: resend three times (no data received yet: heartbeat too)
+    assert [(m.Type, m.SeqNum) for m in sent].count((lsp.MsgType.MsgData, 1)) == 3
+    assert [(m.Type, m.SeqNum) for m in sent].count((lsp.MsgType.MsgAck, 0)) == 3
+    assert lsp.Params().SendCopies == 1  # the library's default: the protocol as specified
 
 
 def test_in_order_delivery_under_reordering_window():

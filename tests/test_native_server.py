@@ -95,23 +95,36 @@ def test_config1_shape(procs, server_bin, miner_bin):
 
 
 def test_many_clients_compiled_and_python_miners_with_drops(procs, server_bin, miner_bin, oracle):
+    """The compiled programs send each datagram in copies (LSP_SEND_COPIES' default, 3),
+    the in-process Python miner and clients once (lsp.Params' default)."""
+    _many_clients(procs, server_bin, miner_bin, oracle)
+
+
+def test_many_clients_with_single_sends_from_the_compiled_programs(procs, plain_server, miner_bin, oracle):
+    """The other way round: the compiled server and miners send every datagram once (the
+    protocol as specified), the Python miner and clients three times."""
+    _many_clients(procs, plain_server, miner_bin, oracle, lsp.Params(EpochLimit=20, EpochMillis=40, WindowSize=1,
+                                                                     SendCopies=3), LSP_SEND_COPIES=1)
+
+
+def _many_clients(procs, server_bin, miner_bin, oracle, params=P, **env):
     import lspnet
     drops = dict(LSPNET_SERVER_READ_DROP=10, LSPNET_SERVER_WRITE_DROP=10)
-    s = System(procs, server_bin, miner_bin, GPUHASH_JOB_SIZE=3000, **drops)
+    s = System(procs, server_bin, miner_bin, GPUHASH_JOB_SIZE=3000, **drops, **env)
     for _ in range(2):
-        s.miner(LSPNET_CLIENT_READ_DROP=10, LSPNET_CLIENT_WRITE_DROP=10)
+        s.miner(LSPNET_CLIENT_READ_DROP=10, LSPNET_CLIENT_WRITE_DROP=10, **env)
 
     class Eng:
         def min(self, msg, lo, hi):
             return oracle.min(msg.encode(), lo, hi)
 
-    threading.Thread(target=bminer.run, args=(f"127.0.0.1:{s.port}", Eng(), P), daemon=True).start()
+    threading.Thread(target=bminer.run, args=(f"127.0.0.1:{s.port}", Eng(), params), daemon=True).start()
     lspnet.SetReadDropPercent(10)
     lspnet.SetWriteDropPercent(10)
     results = {}
 
     def cl(i):
-        results[i] = s.request(f"client-{i:02d}", 20000 + 777 * i)
+        results[i] = bclient.request(f"127.0.0.1:{s.port}", f"client-{i:02d}", 20000 + 777 * i, params)
 
     th = [threading.Thread(target=cl, args=(i,)) for i in range(6)]
     try:

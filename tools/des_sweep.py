@@ -54,10 +54,11 @@ class SplitTail(bserver.Scheduler):
         return size
 
 
-def run(shape: str, policy: dict, seeds: int, epoch_ms: int, drop: float) -> dict:
+def run(shape: str, policy: dict, seeds: int, epoch_ms: int, drop: float, copies: int = 1) -> dict:
     gpus, mpg, nclients, bits, kill = SHAPES[shape]
     params = lsp.NewParams()
     params.EpochMillis = epoch_ms
+    params.SendCopies = copies
     reqs = [(f"client-{i:02d}", 0, 1 << bits) for i in range(nclients)]
     ms, eff, avail, spec, disc = [], [], [], [], []
     for seed in range(seeds):
@@ -70,7 +71,7 @@ def run(shape: str, policy: dict, seeds: int, epoch_ms: int, drop: float) -> dic
         avail.append(r["busy_avail"])
         spec.append(r["speculated"])
     ms.sort()
-    return {"shape": shape, "epoch_ms": epoch_ms, "drop": drop, "policy": policy,
+    return {"shape": shape, "epoch_ms": epoch_ms, "drop": drop, "send_copies": copies, "policy": policy,
             "makespan_mean": round(statistics.mean(ms), 3), "makespan_p90": round(ms[int(0.9 * len(ms))], 3),
             "eff_mean": round(statistics.mean(eff), 4), "busy_avail_mean": round(statistics.mean(avail), 4),
             "busy_avail_min": round(min(avail), 4), "copies_mean": round(statistics.mean(spec), 1),
@@ -87,6 +88,7 @@ def main() -> None:
     ap.add_argument("--seeds", type=int, default=20)
     ap.add_argument("--epoch-ms", type=int, default=2000)
     ap.add_argument("--drop", type=float, default=0.10)
+    ap.add_argument("--copies", default="1", help="LSP SendCopies values, comma-separated")
     args = ap.parse_args()
     if args.policies:
         policies = json.loads(args.policies)
@@ -95,8 +97,9 @@ def main() -> None:
         policies = [dict(job_size=1 << int(b), depth=int(d), **extra)
                     for b in args.sizes.split(",") for d in args.depths.split(",")]
     for shape in args.shapes.split(","):
-        for pol in policies:
-            print(json.dumps(run(shape, pol, args.seeds, args.epoch_ms, args.drop)), flush=True)
+        for copies in (int(c) for c in args.copies.split(",")):
+            for pol in policies:
+                print(json.dumps(run(shape, pol, args.seeds, args.epoch_ms, args.drop, copies)), flush=True)
 
 
 if __name__ == "__main__":

@@ -28,6 +28,7 @@ LIB = os.path.join(ROOT, "bitcoin-miner_amd", "lib")
 NATIVE_MINER = os.path.join(LIB, "gpuhash_miner")
 sys.path.insert(0, os.path.join(ROOT, "bitcoin-miner_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
+from bitcoin import SEND_COPIES  # noqa: E402
 
 
 def free_port() -> int:
@@ -57,10 +58,13 @@ def main() -> None:
                     help="LSP_EPOCH_MILLIS for every program (default: none, the reference's 2000)")
     ap.add_argument("--epoch-limit", type=int, default=None,
                     help="LSP_EPOCH_LIMIT for every program (default: none, the reference's 5)")
+    ap.add_argument("--send-copies", type=int, default=None,
+                    help="LSP_SEND_COPIES for every program (default: none, bitcoin.SEND_COPIES; 1 = as specified)")
     ap.add_argument("--depth", type=int, default=None, help="GPUHASH_MINER_DEPTH (default: the server's)")
     ap.add_argument("--no-backup", action="store_true", help="GPUHASH_BACKUP=0: no speculative copies")
     ap.add_argument("--copies", type=int, default=None, help="GPUHASH_COPIES (default: the server's)")
     ap.add_argument("--label", default="", help="free text copied to the output line")
+    ap.add_argument("--server-log", default=None, help="write the server's stderr here, each line with its time")
     ap.add_argument("--compiled-server", action="store_true",
                     help="the server is lib/gpuhash_server (miners and clients as chosen otherwise)")
     ap.add_argument("--emulate", type=float, default=0.0,
@@ -77,6 +81,8 @@ def main() -> None:
         env["LSP_EPOCH_MILLIS"] = str(args.epoch_ms)
     if args.epoch_limit is not None:
         env["LSP_EPOCH_LIMIT"] = str(args.epoch_limit)
+    if args.send_copies is not None:
+        env["LSP_SEND_COPIES"] = str(args.send_copies)
     port = free_port()
     procs = []
 
@@ -162,6 +168,9 @@ def main() -> None:
                 m.kill()
         time.sleep(0.2)
         log = "\n".join(ln for _, name, ln in lines[server.pid] if name == "err")
+        if args.server_log:
+            with open(args.server_log, "w") as f:
+                f.writelines(f"{t - t0_wall:8.3f} {ln}\n" for t, name, ln in lines[server.pid] if name == "err")
         requeued = log.count("requeued")
         jobs = []  # (miner index, lo, hi, recv, start, end, kernel_s)
         for i, m in enumerate(miners):
@@ -217,7 +226,8 @@ def main() -> None:
                         f"lspnet drop {args.drop}% on every role, "
                         f"{'per-miner jobs (~0.5 s)' if args.adaptive else f'job 2^{args.job_bits}' if args.job_bits else 'default jobs'}, "
                         f"miner killed at {killed}s",
-            "label": args.label, "lsp": {"epoch_ms": args.epoch_ms or 2000, "epoch_limit": args.epoch_limit or 5},
+            "label": args.label, "lsp": {"epoch_ms": args.epoch_ms or 2000, "epoch_limit": args.epoch_limit or 5,
+                                          "send_copies": args.send_copies or SEND_COPIES},
             "depth": args.depth, "backup": not args.no_backup, "emulated_rate": args.emulate or None,
             "wall_s": round(wall, 3), "system_GHs": round(total / wall / 1e9, 3),
             "gpus": ngpus, "jobs": len(jobs), 

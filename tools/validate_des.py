@@ -24,9 +24,11 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 GPU = 34.6e9
 POLICIES = {
-    # name: (system_bench args, Scheduler kwargs for the model)
-    "round5": (["--job-bits", "34", "--depth", "1", "--copies", "1"], dict(job_size=1 << 34, depth=1)),
-    "defaults": ([], None),  # bitcoin.server.make_scheduler(epoch_s=2.0)
+    # name: (system_bench args, Scheduler kwargs for the model (None: make_scheduler's), LSP send copies)
+    "round5": (["--job-bits", "34", "--depth", "1", "--copies", "1", "--send-copies", "1"],
+               dict(job_size=1 << 34, depth=1), 1),
+    "single": (["--send-copies", "1"], None, 1),  # today's scheduler, every datagram sent once
+    "defaults": ([], None, 3),                    # the programs' defaults (bitcoin.SEND_COPIES)
 }
 
 
@@ -52,7 +54,7 @@ def real_run(args, extra: list[str], k: int) -> dict:
 
 
 def model(policy, seeds: int, clients: int, bits: int, client_start: float, miners: int = 1,
-          kill_after: float = -1.0) -> list[dict]:
+          kill_after: float = -1.0, send_copies: int = 1) -> list[dict]:
     import lsp
     import lsp_des
     from bitcoin import server as bserver
@@ -60,8 +62,11 @@ def model(policy, seeds: int, clients: int, bits: int, client_start: float, mine
     kill = (kill_after, miners - 1) if kill_after >= 0 and miners > 1 else None  # system_bench kills the last
     out = []
     for s in range(seeds):
-        sch = bserver.make_scheduler(epoch_s=2.0) if policy is None else bserver.Scheduler(**policy)
-        out.append(lsp_des.run_system(sch, [GPU] * miners, 1, reqs, params=lsp.NewParams(), drop=0.10, seed=s,
+        sch = (bserver.make_scheduler(epoch_s=2.0, send_copies=send_copies) if policy is None
+               else bserver.Scheduler(**policy))
+        params = lsp.NewParams()
+        params.SendCopies = send_copies
+        out.append(lsp_des.run_system(sch, [GPU] * miners, 1, reqs, params=params, drop=0.10, seed=s,
                                       client_start=client_start, kill=kill))
     return out
 
@@ -76,12 +81,12 @@ def main() -> None:
     ap.add_argument("--bits", type=int, default=35)
     ap.add_argument("--miners", type=int, default=1, help="one GPU each (emulated: one 34.6 GH/s miner each)")
     ap.add_argument("--kill-after", type=float, default=-1.0, help="SIGKILL the last miner this long after the clients start")
-    ap.add_argument("--policies", default="round5,defaults")
+    ap.add_argument("--policies", default="round5,single,defaults")
     ap.add_argument("--out", default=None, help="also append each real run's line here")
     ap.add_argument("--compiled-server", action="store_true", help="lib/gpuhash_server instead of bin/server")
     args = ap.parse_args()
     for name in args.policies.split(","):
-        extra, kw = POLICIES[name]
+        extra, kw, send_copies = POLICIES[name]
         def one(k):
             r = real_run(args, extra, k)
             # progress on stdout and the run's line in --out as each run ends (a GPU box
@@ -97,10 +102,10 @@ def main() -> None:
             runs = list(ex.map(one, range(args.runs)))
         # system_bench.py starts the clients 1.5 s (emulated) or 5 s (GPU) after the miners
         sims = model(kw, args.seeds, args.clients, args.bits, 1.5 if args.emulate else 5.0, args.miners,
-                     args.kill_after)
+                     args.kill_after, send_copies)
         work = args.clients * ((1 << args.bits) + 1)
         print(json.dumps({
-            "policy": name, "miners": "emulated (sleep n/34.6e9)" if args.emulate else "GPU",
+            "policy": name, "send_copies": send_copies, "miners": "emulated (sleep n/34.6e9)" if args.emulate else "GPU",
             "server": "lib/gpuhash_server" if args.compiled_server else "bin/server",
             "shape": f"{args.miners} miner(s), {args.clients} clients x [0, 2^{args.bits}], 2 s epochs, limit 5, "
                      f"10% drops" + (f", last miner killed {args.kill_after} s in" if args.kill_after >= 0 else ""),
