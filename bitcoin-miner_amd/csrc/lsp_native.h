@@ -605,12 +605,14 @@ class Udp {
         freeaddrinfo(res);
         peer_ = Addr{a.sin_addr.s_addr, a.sin_port};
         fd_ = socket(AF_INET, SOCK_DGRAM, 0);
+        grow_rcvbuf();
         return fd_ >= 0;
     }
     // server role: a socket bound to the port on every interface (0 = any free port)
     bool listen(int port) {
         fd_ = socket(AF_INET, SOCK_DGRAM, 0);
         if (fd_ < 0) return false;
+        grow_rcvbuf();
         sockaddr_in a{};
         a.sin_family = AF_INET;
         a.sin_addr.s_addr = htonl(INADDR_ANY);
@@ -623,6 +625,13 @@ class Udp {
     }
     int fd() const { return fd_; }
     int port() const { return port_; }
+    // 4 MiB asked of the kernel (granted up to net.core.rmem_max), as lspnet.RCVBUF: a
+    // server takes bursts from every connection at once
+    void grow_rcvbuf() {
+        if (fd_ < 0) return;
+        int bytes = 4 << 20;
+        setsockopt(fd_, SOL_SOCKET, SO_RCVBUF, &bytes, sizeof bytes);
+    }
     const Addr& peer() const { return peer_; }
 
     void write(const std::string& data, const Addr& to) {
@@ -762,11 +771,47 @@ class Conn {
             unacked_.emplace(seq, std::move(payload));
         }
     }
-    // a message this side originates, and the ack of a Data message seen for the first
-    // time, go out copies_ times; a duplicate is acked once (lsp/endpoint.py)
+    // a Data message entering the window, the ack of one seen for the first time, and the
+    // epoch's resends, heartbeat and re-acks go out copies_ times; a duplicate is acked
+    // once (lsp/endpoint.py)
     void send_copies(const LspMsg& m) {
         for (int i = 0; i < copies_; i++) send_(m);
     }
+};
+
+// Recognises the copies of a datagram before they are parsed (lsp/endpoint.py CopyFilter):
+// a datagram whose bytes equal one of the last few from the same address that arrived
+// within min(10 ms, epoch / 20) is a copy, and only the reply its first instance got (the
+// ack of a Data message) is repeated.
+class CopyFilter {
+   public:
+    explicit CopyFilter(double epoch_s) : window_(std::min(0.01, epoch_s / 20)) {}
+    // nullptr for a datagram to handle; for a copy, the reply to repeat (empty: none)
+    const std::string* copy_of(const Addr& a, const std::string& raw) {
+        const double now = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        auto& q = seen_[a];
+        for (auto& e : q)
+            if (e.raw == raw && now - e.t < window_) return &e.reply;
+        q.push_back(Entry{raw, now, {}});
+        if (q.size() > 8) q.pop_front();
+        return nullptr;
+    }
+    // the reply given to the datagram `raw` just handled
+    void reply(const Addr& a, const std::string& raw, std::string r) {
+        auto it = seen_.find(a);
+        if (it != seen_.end() && !it->second.empty() && it->second.back().raw == raw)
+            it->second.back().reply = std::move(r);
+    }
+    void forget(const Addr& a) { seen_.erase(a); }
+
+   private:
+    struct Entry {
+        std::string raw;
+        double t;
+        std::string reply;
+    };
+    double window_;
+    std::map<Addr, std::deque<Entry>> seen_;
 };
 
 // How late the event loop's epochs fire (written under the endpoint's mutex).
@@ -836,7 +881,7 @@ void event_loop(int fd, int epoch_ms, std::mutex& mu, const bool& stop, LoopLate
 
 class Client {
    public:
-    explicit Client(const Params& p) : p_(p), udp_(false) {}
+    explicit Client(const Params& p) : p_(p), udp_(false), copies_(p.epoch_ms / 1000.0) {}
     ~Client() { stop(); }
 
     // Blocks until the server acknowledges the connection (or EpochLimit epochs pass).
@@ -901,6 +946,7 @@ class Client {
     bool stop_ = false, failed_ = false;
     int connect_silent_ = 0;
     LoopLateness late_;
+    CopyFilter copies_;
     std::unique_ptr<Conn> conn_;
     std::deque<std::string> reads_;
 
@@ -922,6 +968,10 @@ class Client {
         Addr from;
         while (udp_.read(raw, from)) {
             if (from != udp_.peer()) continue;
+            if (const std::string* again = copies_.copy_of(from, raw)) {  // a copy
+                if (!again->empty()) udp_.write(*again, from);
+                continue;
+            }
             LspMsg m;
             if (!lsp_unmarshal(raw, m)) continue;
             if (!conn_) {
@@ -935,6 +985,7 @@ class Client {
             }
             if (m.conn != conn_->id()) continue;
             conn_->on_message(m, reads_);
+            if (m.type == MsgData) copies_.reply(from, raw, lsp_marshal(LspMsg{MsgAck, m.conn, m.seq, false, {}}));
             cv_.notify_all();  // delivered data, or acks that may flush a close()
         }
         if (!is_epoch) return;
@@ -964,7 +1015,7 @@ class Server {
         bool timed_out = false;  // read_until: the deadline passed with nothing to return
     };
 
-    explicit Server(const Params& p) : p_(p), udp_(true) {}
+    explicit Server(const Params& p) : p_(p), udp_(true), copies_(p.epoch_ms / 1000.0) {}
     ~Server() { stop(); }
 
     bool listen(int port) {
@@ -1035,6 +1086,7 @@ class Server {
     std::map<long long, Addr> addr_of_;
     std::map<long long, std::unique_ptr<Conn>> conns_;
     std::deque<Event> events_;
+    CopyFilter copies_;
     LoopLateness late_;
 
     void stop() {
@@ -1053,6 +1105,7 @@ class Server {
         auto a = addr_of_.find(id);
         if (a != addr_of_.end()) {
             id_of_.erase(a->second);
+            copies_.forget(a->second);
             addr_of_.erase(a);
         }
         conns_.erase(id);
@@ -1067,6 +1120,10 @@ class Server {
         Addr from;
         std::deque<std::string> got;
         while (udp_.read(raw, from)) {
+            if (const std::string* again = copies_.copy_of(from, raw)) {  // a copy
+                if (!again->empty()) udp_.write(*again, from);
+                continue;
+            }
             LspMsg m;
             if (!lsp_unmarshal(raw, m)) continue;
             if (m.type == MsgConnect) {
@@ -1084,13 +1141,15 @@ class Server {
                     id = it->second;
                     conns_[id]->heard();
                 }
-                udp_.write(lsp_marshal(LspMsg{MsgAck, id, 0, false, {}}), from);
+                for (int i = 0; i < std::max(1, p_.send_copies); i++)
+                    udp_.write(lsp_marshal(LspMsg{MsgAck, id, 0, false, {}}), from);
                 continue;
             }
             auto c = conns_.find(m.conn);
             if (c == conns_.end() || addr_of_[m.conn] != from) continue;
             got.clear();
             c->second->on_message(m, got);
+            if (m.type == MsgData) copies_.reply(from, raw, lsp_marshal(LspMsg{MsgAck, m.conn, m.seq, false, {}}));
             for (auto& p : got) events_.push_back(Event{m.conn, false, std::move(p), {}});
             if (!got.empty()) cv_.notify_all();
         }

@@ -4,11 +4,12 @@ from __future__ import annotations
 
 import queue
 import threading
+import time
 
 import lspnet
 
-from .endpoint import ConnState, Loop
-from .message import Message, MsgType, NewConnect
+from .endpoint import ConnState, CopyFilter, Loop
+from .message import Message, MsgType, NewAck, NewConnect
 from .params import Params, NewParams
 
 
@@ -30,6 +31,7 @@ class Client:
         self._failed = False
         self._closed = False
         self._connect_silent = 0
+        self._copies = CopyFilter(self._p.EpochMillis / 1000.0)
         self.lost_reason = ""
         self._loop = Loop(self._conn, self._p.EpochMillis, self._on_datagram, self._on_command,
                           self._on_epoch, role="lsp-client")
@@ -82,6 +84,11 @@ class Client:
         # socket, which the kernel filters by source (csrc/lsp_native.h does the same)
         if addr != self._conn.peer:
             return
+        again = self._copies.copy_of(addr, data, time.monotonic())
+        if again is not None:  # a copy: repeat the first one's reply
+            if again:
+                self._conn.write_to(again)
+            return
         try:
             m = Message.unmarshal(data)
         except (ValueError, KeyError):
@@ -97,6 +104,8 @@ class Client:
             return
         for payload in self._st.on_message(m):
             self._reads.put(("data", payload))
+        if m.Type == MsgType.MsgData:
+            self._copies.reply(addr, data, NewAck(m.ConnID, m.SeqNum).marshal())
         self._check_close()
 
     def _on_command(self, cmd) -> None:

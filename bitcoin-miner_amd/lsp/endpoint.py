@@ -11,14 +11,17 @@ lsp/server_impl.go, which cannot carry data as written -- SURVEY.md 2 rows 8-9):
     silent unless something arrived; K silent epochs => connection lost.
 
 Send copies (Params.SendCopies, an extension; 1 = the protocol exactly as p1.pdf
-specifies it): every message this side originates -- a Data message when it enters the
-window, the ack of a Data message seen for the first time, and each epoch's resends,
-re-acks and heartbeat -- goes out that many times back to back; a duplicate (a copy, or
-a resend) is acked once.  The receiver already treats the copies as the duplicates an
-epoch resend makes (ack again, deliver once), so the wire protocol is unchanged.  On a
-link that drops each datagram with probability p, a message then holds up its window
-until the next epoch with probability about 2 p^copies (its copies, or the acks of the
-first to arrive, all lost) instead of 1 - (1 - p)^2.
+specifies it): a Connect and its ack, a Data message when it enters the window, the ack
+of a Data message seen for the first time, and each epoch's resends, heartbeat and
+re-acks go out that many times back to back; a duplicate is acked once (lspnet asks for
+a 4 MiB socket receive buffer, so a window of copies from many connections at once is
+not a burst the kernel drops).  Every endpoint recognises a copy
+before parsing it (CopyFilter) and only repeats the reply its first instance got, so a
+copy costs the receiver a bytes comparison.  The wire protocol is unchanged: a copy is
+a duplicate, handled as the protocol's receive rules handle one, and endpoints that send
+once interoperate.  On a link that drops each datagram with probability p, a message
+then holds up its window until the next epoch with probability about 2 p^copies (its
+copies, or all the acks, lost) instead of 1 - (1 - p)^2.
 
 Like the reference's design (one handleMessages goroutine per endpoint), one loop
 thread owns all protocol state; API calls post commands to it through a queue.
@@ -150,6 +153,41 @@ class ConnState:
             self._send_copies(NewData(self.conn_id, seq, self.unacked[seq]))
         for seq in self.recent:
             self._send_copies(NewAck(self.conn_id, seq))
+
+
+class CopyFilter:
+    """Recognises the copies of a datagram before they are parsed.  A peer that sends
+    copies (SendCopies) sends them back to back, so a datagram whose bytes equal one of
+    the last few from the same address that arrived within `window` seconds is a copy: its
+    first instance has been handled, and the receiver only repeats the reply it gave that
+    one (the ack of a Data message; nothing for anything else), as the protocol's rule for
+    a duplicate says, without parsing it again.  An epoch resend arrives an epoch later
+    and is handled in full."""
+
+    def __init__(self, epoch_s: float, depth: int = 8):
+        self.window = min(0.01, epoch_s / 20)
+        self.depth = depth
+        self.seen: dict = {}  # addr -> deque of [raw bytes, arrival time, reply bytes]
+
+    def copy_of(self, addr, raw: bytes, now: float):
+        """None for a datagram to handle; for a copy, the reply to repeat (b"": none)."""
+        q = self.seen.get(addr)
+        if q is None:
+            q = self.seen[addr] = collections.deque(maxlen=self.depth)
+        for e in q:
+            if e[0] == raw and now - e[1] < self.window:
+                return e[2]
+        q.append([raw, now, b""])
+        return None
+
+    def reply(self, addr, raw: bytes, reply: bytes) -> None:
+        """Records the reply given to the datagram `raw` just handled."""
+        q = self.seen.get(addr)
+        if q and q[-1][0] == raw:
+            q[-1][2] = reply
+
+    def forget(self, addr) -> None:
+        self.seen.pop(addr, None)
 
 
 class Loop:

@@ -13,7 +13,7 @@ import time
 import lspnet
 
 from .client import LSPError
-from .endpoint import ConnState, Loop
+from .endpoint import ConnState, CopyFilter, Loop
 from .message import Message, MsgType, NewAck
 from .params import Params, NewParams
 
@@ -29,6 +29,7 @@ class Server:
         self._id_of: dict[tuple, int] = {}
         self._next_id = 1
         self._closing_all = False
+        self._copies = CopyFilter(self._p.EpochMillis / 1000.0)
         self._done = threading.Event()
         self._closed = False
         self._lost_during_close = False
@@ -93,6 +94,11 @@ class Server:
         return lambda m: self._conn.write_to(m.marshal(), addr)
 
     def _on_datagram(self, data: bytes, addr) -> None:
+        again = self._copies.copy_of(addr, data, time.monotonic())
+        if again is not None:  # a copy: repeat the first one's reply
+            if again:
+                self._conn.write_to(again, addr)
+            return
         try:
             m = Message.unmarshal(data)
         except (ValueError, KeyError):
@@ -111,13 +117,16 @@ class Server:
             st = self._conns.get(cid)
             if st is not None:
                 st.mark_heard()
-                self._conn.write_to(NewAck(cid, 0).marshal(), addr)
+                for _ in range(max(1, self._p.SendCopies)):
+                    self._conn.write_to(NewAck(cid, 0).marshal(), addr)
             return
         st = self._conns.get(m.ConnID)
         if st is None or self._addr_of.get(m.ConnID) != addr:
             return
         for payload in st.on_message(m):
             self._reads.put(("data", m.ConnID, payload))
+        if m.Type == MsgType.MsgData:
+            self._copies.reply(addr, data, NewAck(m.ConnID, m.SeqNum).marshal())
         self._reap()
 
     def _on_command(self, cmd) -> None:
@@ -161,6 +170,7 @@ class Server:
         addr = self._addr_of.pop(cid, None)
         if addr is not None:
             self._id_of.pop(addr, None)
+            self._copies.forget(addr)
 
 
 def NewServer(port: int, params: Params | None = None) -> Server:

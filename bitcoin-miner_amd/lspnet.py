@@ -113,8 +113,24 @@ def resolve(hostport: str):
     return (socket.gethostbyname(host or "127.0.0.1"), int(port))
 
 
-def ListenUDP(port: int, host: str = "0.0.0.0") -> UDPConn:
+# Receive buffer asked of the kernel (it grants at most net.core.rmem_max): a server's
+# socket takes bursts from every connection at once -- each epoch's resends and re-acks,
+# and a window of Data messages in send copies -- and the default ~200 KB holds only a
+# couple of hundred small datagrams.
+RCVBUF = 4 << 20
+
+
+def _udp_socket() -> socket.socket:
     s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    try:
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, RCVBUF)
+    except OSError:
+        pass
+    return s
+
+
+def ListenUDP(port: int, host: str = "0.0.0.0") -> UDPConn:
+    s = _udp_socket()
     s.bind((host, int(port)))
     s.setblocking(False)
     return UDPConn(s, "server")
@@ -122,7 +138,7 @@ def ListenUDP(port: int, host: str = "0.0.0.0") -> UDPConn:
 
 def DialUDP(hostport: str) -> UDPConn:
     peer = resolve(hostport)
-    s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    s = _udp_socket()
     s.bind(("0.0.0.0", 0))
     s.setblocking(False)
     return UDPConn(s, "client", peer)

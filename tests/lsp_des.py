@@ -4,7 +4,8 @@ state machine, for sizing the server's jobs on lossy links.
 Test infrastructure (tests/test_scheduler_sim.py, tools/des_sweep.py), not product code.
 What is real and what is modelled:
   * REAL: each connection end is lsp.endpoint.ConnState (window, in-order delivery, acks,
-    epoch resends and re-acks, loss after EpochLimit silent epochs), the connect
+    epoch resends and re-acks, loss after EpochLimit silent epochs, send copies) behind
+    lsp.endpoint.CopyFilter, the connect
     handshake follows lsp/client.py and lsp/server.py, and the server is
     bitcoin.server.ServerCore over its Scheduler -- the code the server program runs;
   * MODELLED: the network (each datagram is dropped at the sender with the role's write
@@ -25,7 +26,7 @@ import lsp
 from bitcoin import MsgType as BMsg
 from bitcoin import NewJoin, NewRequest, NewResult, marshal, unmarshal
 from bitcoin import server as bserver
-from lsp.endpoint import ConnState
+from lsp.endpoint import ConnState, CopyFilter
 from lsp.message import MsgType, NewAck, NewConnect
 
 
@@ -69,7 +70,16 @@ class Net:
     def _arrive(self, src, dst, msg) -> None:
         if dst.dead or self.sim.rng.random() < dst.rdrop:
             return
+        # lsp.endpoint.CopyFilter: a copy only repeats its first instance's reply
+        raw = (msg.Type, msg.ConnID, msg.SeqNum, msg.Payload)
+        again = dst.copies.copy_of(id(src), raw, self.sim.t)
+        if again is not None:
+            if again:
+                self.send(dst, src, again)
+            return
         dst.on_datagram(src, msg)
+        if msg.Type == MsgType.MsgData:
+            dst.copies.reply(id(src), raw, NewAck(msg.ConnID, msg.SeqNum))
 
 
 class Endpoint:
@@ -78,6 +88,7 @@ class Endpoint:
         self.rdrop, self.wdrop = rdrop, wdrop
         self.dead = False
         self.epoch = params.EpochMillis / 1000.0
+        self.copies = CopyFilter(self.epoch)
         sim.at(sim.t + self.epoch, self._epoch)
 
     def _epoch(self) -> None:
@@ -112,7 +123,8 @@ class ServerEP(Endpoint):
             st = self.conns.get(cid)
             if st is not None:
                 st.mark_heard()
-                self.net.send(self, src, NewAck(cid, 0))
+                for _ in range(max(1, self.p.SendCopies)):
+                    self.net.send(self, src, NewAck(cid, 0))
             return
         st = self.conns.get(m.ConnID)
         if st is None or self.peer.get(m.ConnID) is not src:

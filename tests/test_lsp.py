@@ -133,7 +133,7 @@ def test_send_copies_count():
     b_sent.clear()
     b.on_epoch()  # re-ack the last received message, three times
     assert [(m.Type, m.SeqNum) for m in b_sent] == [(lsp.MsgType.MsgAck, 1)] * 3
-    a.on_epoch()  # unacked: resend three times (no data received yet: heartbeat too)
+    a.on_epoch()  # unacked: resent three times; no data received yet: heartbeat too
     assert [(m.Type, m.SeqNum) for m in sent].count((lsp.MsgType.MsgData, 1)) == 3
     assert [(m.Type, m.SeqNum) for m in sent].count((lsp.MsgType.MsgAck, 0)) == 3
     assert lsp.Params().SendCopies == 1  # the library's default: the protocol as specified
