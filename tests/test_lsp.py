@@ -257,3 +257,21 @@ def test_client_hears_only_its_server():
         srv.Close()
     except lsp.LSPError:
         pass
+
+
+def test_copy_filter():
+    """lsp.endpoint.CopyFilter: the same bytes from the same address within min(10 ms,
+    epoch / 20) are a copy, answered with the reply its first instance got; a resend an
+    epoch later, or the same bytes from another address, are handled in full."""
+    from lsp.endpoint import CopyFilter
+    f = CopyFilter(2.0)
+    a, b = ("127.0.0.1", 1), ("127.0.0.1", 2)
+    assert f.copy_of(a, b"d1", 100.0) is None
+    f.reply(a, b"d1", b"ack1")
+    assert f.copy_of(a, b"d1", 100.001) == b"ack1"
+    assert f.copy_of(b, b"d1", 100.001) is None          # another peer
+    assert f.copy_of(a, b"d1", 102.0) is None            # an epoch resend
+    assert f.copy_of(a, b"h0", 102.0) is None and f.copy_of(a, b"h0", 102.0) == b""  # no reply
+    f.forget(a)
+    assert f.copy_of(a, b"h0", 102.0) is None
+    assert CopyFilter(0.04).window == pytest.approx(0.002)
