@@ -2,7 +2,7 @@
 # tools/gpu_session.sh STEP... -- runs GPU steps on the gpurun box, each under its own
 # time limit, logging to gpurun_out/.  A plain failure (exit 1, e.g. a failing test)
 # lets the next step run; a fault, abort, segfault, time limit or kill stops the session.
-# Steps: valid | validcopies | valid37 | c5ref | c5diag200 | hostwait | c5diag | c5stream | c5poll | lsweep | inproc8s | dist8s | fma | cumask | family | inproc8c4 | valu | go | test | soak | smoke | bench | bench3 | bench4 | prof4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | pmc3 | pmc4 | sweep | variants | partial | regret | sys5
+# Steps: valid | validcopies | validcopies37 | valid37 | c5ref | c5diag200 | hostwait | c5diag | c5stream | c5poll | lsweep | inproc8s | dist8s | fma | cumask | family | inproc8c4 | valu | go | test | soak | smoke | bench | bench3 | bench4 | prof4 | c4full | dist8c4 | dist2 | inproc | latency | prof | pmc | pmc3 | pmc4 | sweep | variants | partial | regret | sys5
 set -u
 cd "$(dirname "$0")/.."
 OUT=gpurun_out
@@ -38,6 +38,7 @@ for step in "$@"; do
         valid) run validate_des 900 python -u tools/validate_des.py --runs "${VALID_RUNS:-10}" --out "$OUT/r06_validate_des_runs.jsonl" ;;
         validnew) run validate_des_defaults 900 python -u tools/validate_des.py --runs "${VALID_RUNS:-10}" --policies defaults --out "$OUT/r06_validate_des_runs_defaults2.jsonl" ;;
         validcopies) run validate_des_copies 900 python -u tools/validate_des.py --runs "${VALID_RUNS:-10}" --policies single,defaults --out "$OUT/r06_validate_des_runs_copies.jsonl" ;;
+        validcopies37) run validate_des_copies_2p37 600 python -u tools/validate_des.py --runs "${VALID_RUNS:-4}" --bits 37 --seeds 100 --policies single,defaults --out "$OUT/r06_validate_des_runs_copies_2p37.jsonl" ;;
         valid37) run validate_des_2p37 600 python -u tools/validate_des.py --runs "${VALID_RUNS:-4}" --bits 37 --seeds 100 --out "$OUT/r06_validate_des_runs_2p37.jsonl" ;;
         killprobe) run kill_probe 400 python -u tools/kill_probe.py --rounds "${KILL_ROUNDS:-4}" ;;
         c5ref) run c5ref 500 env GPUHASH_DIAG_DIR="$OUT/c5ref" python -u -m pytest tests/test_gpu_system.py -m gpu -x -v -s --timeout 450 --timeout-method thread -k reference_lsp_params ;;
