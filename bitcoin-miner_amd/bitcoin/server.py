@@ -571,6 +571,11 @@ def serve(port: int, params=None, job_size: int | None = None, ready=None, log=N
         ready(srv)
     sched = make_scheduler(job_size, params.EpochMillis / 1000.0, params.SendCopies)
     core = ServerCore(sched, srv.Write, srv.CloseConn, log)
+    if log:  # the configuration, in the words of csrc/server_main.cpp (tests compare the two)
+        size = "per-miner" if sched.sizing is not None else str(sched.job_size)
+        log(f"config: jobs of {size} nonces, depth {sched.depth}, {sched.copies} live copies of an overdue "
+            f"job; LSP epoch {params.EpochMillis} ms, limit {params.EpochLimit}, window {params.WindowSize}, "
+            f"send copies {params.SendCopies}")
     while True:
         wake = core.sched.next_wakeup()
         try:

@@ -456,6 +456,12 @@ int main(int argc, char** argv) {
     Scheduler sched(env_u64("GPUHASH_JOB_SIZE", default_job_size(params.epoch_ms / 1000.0, params.send_copies)),
                     (int)env_u64("GPUHASH_MINER_DEPTH", kDefaultDepth),
                     copies, kSlack, kSlackFrac);
+    // the configuration, in the words of server.py's serve() (tests compare the two)
+    logf("config: jobs of %llu nonces, depth %d, %d live copies of an overdue job; LSP epoch %d ms, limit %d, "
+         "window %d, send copies %d",
+         (unsigned long long)env_u64("GPUHASH_JOB_SIZE", default_job_size(params.epoch_ms / 1000.0, params.send_copies)),
+         (int)env_u64("GPUHASH_MINER_DEPTH", kDefaultDepth), copies, params.epoch_ms, params.epoch_limit,
+         params.window, params.send_copies);
 
     auto dispatch = [&] {
         while (!sched.abandoned.empty()) {

@@ -10,6 +10,7 @@ all-compiled system (this server, lib/gpuhash_miner on the GPU) end to end.
 import os
 import signal
 import subprocess
+import sys
 import threading
 import time
 
@@ -374,3 +375,35 @@ def _overdue_case(procs, plain_server, miner_bin, oracle, which):
 def bserver_serve(params, job_size, holder, log):
     from bitcoin import server as bserver
     bserver.serve(0, params=params, job_size=job_size, ready=lambda srv: holder.setdefault("srv", srv), log=log)
+
+
+@pytest.mark.parametrize("lsp_env", [{}, {"LSP_SEND_COPIES": "1"}, {"LSP_EPOCH_MILLIS": "200"},
+                                     {"LSP_EPOCH_MILLIS": "40", "LSP_EPOCH_LIMIT": "20", "LSP_SEND_COPIES": "2"},
+                                     {"GPUHASH_JOB_SIZE": "12345", "GPUHASH_MINER_DEPTH": "2", "GPUHASH_BACKUP": "0"}],
+                         ids=["reference_params", "single_sends", "200ms", "40ms_two_copies", "overrides"])
+def test_compiled_and_python_servers_choose_the_same_defaults(procs, plain_server, lsp_env):
+    """Both servers log their configuration at start; for the same environment the lines
+    are identical: job size (server.py default_job_size / server_main.cpp's mirror, from
+    the epoch and the send copies), depth, speculative copies and the LSP parameters."""
+    server_py = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                             "bitcoin-miner_amd", "bin", "server")
+    base = {k: v for k, v in os.environ.items() if not k.startswith(("LSP_", "GPUHASH_"))}
+    lines = []
+    for argv in ([plain_server], [sys.executable, server_py]):
+        env = dict(base, GPUHASH_SERVER_LOG="1", **lsp_env)
+        p = subprocess.Popen(argv + [str(free_port())], env=env, stdout=subprocess.PIPE,
+                             stderr=subprocess.PIPE, text=True)
+        procs.ps.append(p)
+        line = ""
+        deadline = time.monotonic() + 30
+        while time.monotonic() < deadline and "config:" not in line:
+            line = p.stderr.readline()
+        p.terminate()
+        p.wait(10)
+        assert "config:" in line, (argv, line)
+        lines.append(line.strip())
+    assert lines[0] == lines[1], lines
+    if not lsp_env:
+        assert "jobs of 17179869184 nonces, depth 3, 3 live copies" in lines[0] and "send copies 3" in lines[0]
+    if lsp_env == {"LSP_SEND_COPIES": "1"}:
+        assert "jobs of 68719476736 nonces" in lines[0]
